@@ -1,0 +1,182 @@
+/* include/rt_mi355x.h -- C ABI of librt_mi355x.so, the MI355X (gfx950) render
+ * path for caidj0/Raytracer-2025.
+ *
+ * The reference path is `Camera::render(&mut self, world: &dyn Hittable,
+ * lights: Option<&dyn Hittable>) -> RgbImage` (src/camera.rs:161) over the
+ * plugin traits Hittable (src/hit.rs:46-60), Material (src/material.rs:23-34),
+ * Texture (src/texture.rs:5-7) and PDF (src/pdf.rs:13-16).  Rust trait objects
+ * cannot cross a C boundary, so the world is described by constructor calls
+ * that mirror the reference constructors one-to-one (each cited below), and is
+ * flattened once into device arrays at the first rt_render that uses it.
+ *
+ * Conventions
+ *  - Every constructor returns a handle >= 0 or a negative RT_E* code; the
+ *    message of the last failure on this thread is rt_last_error().
+ *  - Handles are per scene and per kind (texture / material / object).
+ *    Textures and materials are shared (Arc in the reference): a handle may be
+ *    used any number of times.  Objects are owned (Box<dyn Hittable>): passing
+ *    an object to rt_hittables_add / rt_bvh_new / rt_transform_new /
+ *    rt_constant_medium_new moves it, and a moved handle is RT_EMOVED
+ *    afterwards (the Rust compiler rejects such reuse).
+ *  - Reference panics (assert!, expect, unwrap, unimplemented!) become
+ *    RT_EPANIC with a message; the library never aborts the process.
+ *  - Not thread-safe per scene: calls on one scene are serialised by the
+ *    caller.  Different scenes may be used from different threads.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum rt_status {
+    RT_OK = 0,
+    RT_EINVAL = -1,       /* bad argument (null pointer, non-finite, out of range) */
+    RT_EHANDLE = -2,      /* unknown handle or wrong kind */
+    RT_EMOVED = -3,       /* object handle already moved into another object */
+    RT_EDEGENERATE = -4,  /* Triangle::new returned None (triangle.rs:29-31) */
+    RT_EPANIC = -5,       /* a reference panic condition was hit (message in rt_last_error) */
+    RT_EUNSUPPORTED = -6, /* construct valid in the reference but not on this path yet */
+    RT_EDEVICE = -7,      /* HIP runtime error, or no gfx950 device */
+    RT_ENOMEM = -8,       /* host or device allocation failed */
+    RT_ESTACK = -9        /* world deeper than the kernel's traversal stack */
+};
+
+typedef struct rt_scene rt_scene;
+
+int32_t rt_abi_version(void);
+const char* rt_last_error(void);
+rt_scene* rt_scene_create(void);
+void rt_scene_destroy(rt_scene* s);
+
+/* ---- Textures (src/texture.rs) ------------------------------------------ */
+/* SolidColor::new (texture.rs:14-16) */
+int32_t rt_tex_solid(rt_scene* s, const double rgb[3]);
+/* CheckerTexture::new (texture.rs:46-56) */
+int32_t rt_tex_checker(rt_scene* s, double scale, int32_t even_tex, int32_t odd_tex);
+/* ImageTexture::new / new_raw_image (texture.rs:82-97): pixels already decoded
+ * to linear RGBA f32, row 0 = top (image.rs:63-82).  width == height == 0 is a
+ * missing file: value() is cyan (texture.rs:167-169).  linear_interp selects
+ * ImageInterpMethod::Linear (new_raw_image) instead of None. */
+int32_t rt_tex_image(rt_scene* s, uint32_t width, uint32_t height, const float* rgba, int32_t linear_interp);
+/* NoiseTexture::new (texture.rs:183-188).  Perlin tables are drawn from
+ * SplitMix64(seed) in the order of perlin.rs:16-36. */
+int32_t rt_tex_noise(rt_scene* s, double scale, uint64_t seed);
+/* Book-1 sky: a user Texture for Camera.background (camera.rs:50) with
+ * value(u,v,p) = (1-a)*horizon + a*zenith, a = (p.y+1)/2, p = unit direction
+ * (environment.rs:14-24).  Not a reference type: the reference has no book-1
+ * sky, so the build defines it through the Texture trait. */
+int32_t rt_tex_sky_gradient(rt_scene* s, const double horizon[3], const double zenith[3]);
+
+/* ---- Materials (src/material.rs) ---------------------------------------- */
+int32_t rt_mat_empty(rt_scene* s);                                         /* EmptyMaterial 36-47 */
+int32_t rt_mat_lambertian(rt_scene* s, int32_t tex);                       /* Lambertian::new 53-57 */
+int32_t rt_mat_metal(rt_scene* s, const double albedo[3], double fuzz);   /* Metal::new 73-80 */
+int32_t rt_mat_dielectric(rt_scene* s, int32_t tex, double ior);          /* Dielectric::new 103-108 */
+/* DiffuseLight::new / new_with_material (152-169); inner_mat -1 = None */
+int32_t rt_mat_diffuse_light(rt_scene* s, int32_t tex, int32_t inner_mat);
+int32_t rt_mat_isotropic(rt_scene* s, int32_t tex);                        /* Isotropic::new 193-197 */
+int32_t rt_mat_transparent(rt_scene* s);                                   /* Transparent 209-218 */
+int32_t rt_mat_mix(rt_scene* s, int32_t mat1, int32_t mat2, double ratio); /* Mix::new 227-233 */
+
+/* ---- Hittables ------------------------------------------------------------ */
+/* Sphere::new (shapes/sphere.rs:25-35) */
+int32_t rt_sphere(rt_scene* s, const double center[3], double radius, int32_t mat);
+/* Sphere::new_with_motion (shapes/sphere.rs:37-51) */
+int32_t rt_sphere_moving(rt_scene* s, const double center1[3], const double center2[3], double radius, int32_t mat);
+/* Quad::new (shapes/quad.rs:30-47) */
+int32_t rt_quad(rt_scene* s, const double anchor[3], const double u[3], const double v[3], int32_t mat);
+/* Triangle::new (shapes/triangle.rs:28-46); RT_EDEGENERATE where it returns None */
+int32_t rt_triangle(rt_scene* s, const double anchor[3], const double u[3], const double v[3], int32_t mat);
+/* Hittables::default (hits.rs:9) -- an empty list object */
+int32_t rt_hittables_new(rt_scene* s);
+/* Hittables::add (hits.rs:27-30); moves `object` */
+int32_t rt_hittables_add(rt_scene* s, int32_t list, int32_t object);
+/* BVH::new(Hittables) (bvh.rs:12-46); moves `list`; same topology as the reference */
+int32_t rt_bvh_new(rt_scene* s, int32_t list);
+/* build_box (shapes/quad.rs:128-189); returns a Hittables object */
+int32_t rt_build_box(rt_scene* s, const double a[3], const double b[3], int32_t mat);
+/* Transform::new (shapes.rs:31-47); moves `object`; null pointers = None
+ * (offset 0, identity quaternion (w,x,y,z), scale 1) */
+int32_t rt_transform_new(rt_scene* s, int32_t object, const double* offset3, const double* quat_wxyz, const double* scale3);
+/* ConstantMedium::new_with_tex (volume.rs:23-33); moves `boundary` */
+int32_t rt_constant_medium_new(rt_scene* s, int32_t boundary, double density, int32_t tex);
+
+/* Quaternion::from_axis_angle / from_euler (utils/quaternion.rs:23-53), host helpers */
+int32_t rt_quat_from_axis_angle(const double axis[3], double angle_degrees, double out_wxyz[4]);
+void rt_quat_from_euler(double yaw, double pitch, double roll, double out_wxyz[4]);
+
+/* ---- Camera (src/camera.rs:45-61 pub fields) ------------------------------ */
+typedef struct rt_camera {
+    double aspect_ratio;
+    uint32_t image_width;
+    uint32_t samples_per_pixel; /* traced samples = floor(sqrt(spp))^2 (camera.rs:212) */
+    uint32_t max_depth;
+    int32_t background_tex; /* Environment texture; -1 = SolidColor(BLACK) (camera.rs:83-85) */
+    double vertical_fov_in_degrees;
+    double look_from[3];
+    double look_at[3];
+    double vec_up[3];
+    double defocus_angle_in_degrees;
+    double focus_distance;
+    int32_t toon_map; /* 0 = ToonMap::None, 1 = ToonMap::ACES (utils/color.rs:8-11) */
+    int32_t reserved;
+} rt_camera;
+
+/* Camera::default (camera.rs:76-104) */
+void rt_camera_default(rt_camera* cam);
+/* Camera::initilize's image_height (camera.rs:205-210) */
+uint32_t rt_camera_image_height(const rt_camera* cam);
+
+typedef struct rt_render_opts {
+    uint64_t seed;       /* render RNG key (oracle/rng_contract.hpp) */
+    uint32_t row_offset; /* shard: render rows y = row_offset + k*row_stride */
+    uint32_t row_stride; /* 0 or 1 = every row */
+    uint32_t threads;    /* CPU implementations only; 0 = all cores */
+    uint32_t flags;      /* reserved, 0 */
+    void* stream;        /* hipStream_t for rt_render_device; NULL = default */
+} rt_render_opts;
+
+void rt_render_opts_default(rt_render_opts* opts);
+
+typedef struct rt_stats {
+    uint64_t samples;         /* traced camera samples (pixels x floor(sqrt(spp))^2) */
+    uint64_t rays;            /* ray_color calls that reached world.hit */
+    uint64_t panics;          /* reference assert/expect conditions (NaN, zero pdf, ...) */
+    uint64_t reserved0;
+    double render_ms;         /* wall time of the call (host) */
+    double kernel_ms;         /* device time of the path-tracing kernel (HIP events) */
+    double flatten_ms;        /* world flatten + upload, 0 when cached */
+    double reserved1;
+} rt_stats;
+
+/* Camera::render(&world, lights) (camera.rs:161-202).  world: object handle;
+ * lights: object handle or -1 (None).  Writes the shard's rows, compact and
+ * row-major (y down), as linear RGB f32 = pixel_color * pixel_sample_scale
+ * (camera.rs:193) to out_linear_rgb (rows x W x 3, may be NULL) and as sRGB u8
+ * = Color::to_rgb (utils/color.rs:27-36) to out_srgb (may be NULL).  Blocking.
+ * Objects passed here are borrowed, not moved. */
+int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
+                  float* out_linear_rgb, uint8_t* out_srgb, rt_stats* stats);
+
+/* Number of rows a shard renders (rows of the compact output). */
+uint32_t rt_shard_rows(const rt_camera* cam, const rt_render_opts* opts);
+
+/* Device-resident variant: out_linear_rgb_device is a gfx950 device pointer
+ * (rows x W x 3 f32).  Enqueued on opts->stream and returns without waiting;
+ * stats (if given) are filled by rt_render_device_wait. */
+int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam,
+                         const rt_render_opts* opts, float* out_linear_rgb_device);
+/* Waits for the last rt_render_device on this scene and reports its stats. */
+int32_t rt_render_device_wait(rt_scene* s, rt_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

@@ -1,0 +1,335 @@
+// oracle/rt_oracle_capi.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// The C ABI of include/rt_mi355x.h implemented by the CPU oracle under the
+// prefix `orc_` (liboracle.so), so tests can build one scene description on
+// both the gfx950 library and the oracle and compare the images.
+#include <cstdio>
+#include <mutex>
+#include <thread>
+
+#include "../include/rt_mi355x.h"
+#include "rt_oracle.hpp"
+
+using namespace orc;
+
+namespace {
+thread_local std::string g_err;
+
+int32_t fail(int32_t code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+Vec3 v3(const double* p) { return Vec3(p[0], p[1], p[2]); }
+
+}  // namespace
+
+struct rt_scene {
+    std::vector<std::shared_ptr<Texture>> tex;
+    std::vector<std::shared_ptr<Material>> mat;
+    std::vector<HittablePtr> obj;  // null after a move
+    std::vector<bool> moved;
+    uint32_t next_medium_id = 0;
+
+    int32_t add_obj(HittablePtr p) {
+        obj.push_back(std::move(p));
+        moved.push_back(false);
+        return (int32_t)obj.size() - 1;
+    }
+    bool tex_ok(int32_t t) const { return t >= 0 && (size_t)t < tex.size(); }
+    bool mat_ok(int32_t m) const { return m >= 0 && (size_t)m < mat.size(); }
+    int32_t check_obj(int32_t o) const {
+        if (o < 0 || (size_t)o >= obj.size()) return fail(RT_EHANDLE, "unknown object handle");
+        if (moved[o]) return fail(RT_EMOVED, "object handle already moved");
+        return RT_OK;
+    }
+    HittablePtr take(int32_t o) {
+        moved[o] = true;
+        return std::move(obj[o]);
+    }
+};
+
+#define GUARD_BEGIN try {
+#define GUARD_END                                          \
+    }                                                      \
+    catch (const Panic& p) {                               \
+        return fail(RT_EPANIC, p.what());                  \
+    }                                                      \
+    catch (const std::bad_alloc&) {                        \
+        return fail(RT_ENOMEM, "out of memory");           \
+    }                                                      \
+    catch (const std::exception& e) {                      \
+        return fail(RT_EINVAL, e.what());                  \
+    }
+
+extern "C" {
+
+int32_t orc_abi_version(void) { return RT_ABI_VERSION; }
+const char* orc_last_error(void) { return g_err.c_str(); }
+rt_scene* orc_scene_create(void) { return new rt_scene(); }
+void orc_scene_destroy(rt_scene* s) { delete s; }
+
+int32_t orc_tex_solid(rt_scene* s, const double rgb[3]) {
+    if (!s || !rgb) return fail(RT_EINVAL, "null");
+    s->tex.push_back(std::make_shared<SolidColor>(v3(rgb)));
+    return (int32_t)s->tex.size() - 1;
+}
+int32_t orc_tex_checker(rt_scene* s, double scale, int32_t even, int32_t odd) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->tex_ok(even) || !s->tex_ok(odd)) return fail(RT_EHANDLE, "unknown texture");
+    s->tex.push_back(std::make_shared<CheckerTexture>(scale, s->tex[even], s->tex[odd]));
+    return (int32_t)s->tex.size() - 1;
+}
+int32_t orc_tex_image(rt_scene* s, uint32_t w, uint32_t h, const float* rgba, int32_t linear) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if ((w == 0) != (h == 0)) return fail(RT_EINVAL, "image must have both dimensions or none");
+    if (w && !rgba) return fail(RT_EINVAL, "null pixels");
+    auto t = std::make_shared<ImageTexture>();
+    t->w = (int)w;
+    t->h = (int)h;
+    t->linear_interp = linear != 0;
+    if (w) t->rgba.assign(rgba, rgba + (size_t)w * h * 4);
+    s->tex.push_back(t);
+    return (int32_t)s->tex.size() - 1;
+}
+int32_t orc_tex_noise(rt_scene* s, double scale, uint64_t seed) {
+    if (!s) return fail(RT_EINVAL, "null");
+    s->tex.push_back(std::make_shared<NoiseTexture>(scale, seed));
+    return (int32_t)s->tex.size() - 1;
+}
+int32_t orc_tex_sky_gradient(rt_scene* s, const double horizon[3], const double zenith[3]) {
+    if (!s || !horizon || !zenith) return fail(RT_EINVAL, "null");
+    s->tex.push_back(std::make_shared<SkyGradient>(v3(horizon), v3(zenith)));
+    return (int32_t)s->tex.size() - 1;
+}
+
+static int32_t push_mat(rt_scene* s, std::shared_ptr<Material> m) {
+    s->mat.push_back(std::move(m));
+    return (int32_t)s->mat.size() - 1;
+}
+int32_t orc_mat_empty(rt_scene* s) { return s ? push_mat(s, std::make_shared<EmptyMaterial>()) : fail(RT_EINVAL, "null"); }
+int32_t orc_mat_lambertian(rt_scene* s, int32_t tex) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
+    return push_mat(s, std::make_shared<Lambertian>(s->tex[tex]));
+}
+int32_t orc_mat_metal(rt_scene* s, const double albedo[3], double fuzz) {
+    if (!s || !albedo) return fail(RT_EINVAL, "null");
+    return push_mat(s, std::make_shared<Metal>(v3(albedo), fuzz));
+}
+int32_t orc_mat_dielectric(rt_scene* s, int32_t tex, double ior) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
+    return push_mat(s, std::make_shared<Dielectric>(s->tex[tex], ior));
+}
+int32_t orc_mat_diffuse_light(rt_scene* s, int32_t tex, int32_t inner) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
+    if (inner != -1 && !s->mat_ok(inner)) return fail(RT_EHANDLE, "unknown material");
+    return push_mat(s, std::make_shared<DiffuseLight>(s->tex[tex], inner == -1 ? nullptr : s->mat[inner]));
+}
+int32_t orc_mat_isotropic(rt_scene* s, int32_t tex) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
+    return push_mat(s, std::make_shared<Isotropic>(s->tex[tex]));
+}
+int32_t orc_mat_transparent(rt_scene* s) { return s ? push_mat(s, std::make_shared<Transparent>()) : fail(RT_EINVAL, "null"); }
+int32_t orc_mat_mix(rt_scene* s, int32_t m1, int32_t m2, double ratio) {
+    if (!s) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(m1) || !s->mat_ok(m2)) return fail(RT_EHANDLE, "unknown material");
+    return push_mat(s, std::make_shared<Mix>(s->mat[m1], s->mat[m2], ratio));
+}
+
+int32_t orc_sphere(rt_scene* s, const double c[3], double r, int32_t mat) {
+    if (!s || !c) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(mat)) return fail(RT_EHANDLE, "unknown material");
+    return s->add_obj(std::make_unique<Sphere>(v3(c), r, s->mat[mat]));
+}
+int32_t orc_sphere_moving(rt_scene* s, const double c1[3], const double c2[3], double r, int32_t mat) {
+    if (!s || !c1 || !c2) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(mat)) return fail(RT_EHANDLE, "unknown material");
+    return s->add_obj(std::make_unique<Sphere>(v3(c1), v3(c2), r, s->mat[mat]));
+}
+int32_t orc_quad(rt_scene* s, const double q[3], const double u[3], const double v[3], int32_t mat) {
+    if (!s || !q || !u || !v) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(mat)) return fail(RT_EHANDLE, "unknown material");
+    GUARD_BEGIN
+    return s->add_obj(make_quad(v3(q), v3(u), v3(v), s->mat[mat]));
+    GUARD_END
+}
+int32_t orc_triangle(rt_scene* s, const double a[3], const double u[3], const double v[3], int32_t mat) {
+    if (!s || !a || !u || !v) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(mat)) return fail(RT_EHANDLE, "unknown material");
+    auto t = make_triangle(v3(a), v3(u), v3(v), s->mat[mat]);
+    if (!t) return fail(RT_EDEGENERATE, "degenerate triangle (Triangle::new -> None)");
+    return s->add_obj(std::move(t));
+}
+int32_t orc_hittables_new(rt_scene* s) {
+    if (!s) return fail(RT_EINVAL, "null");
+    return s->add_obj(std::make_unique<Hittables>());
+}
+int32_t orc_hittables_add(rt_scene* s, int32_t list, int32_t object) {
+    if (!s) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(list)) != RT_OK) return rc;
+    if ((rc = s->check_obj(object)) != RT_OK) return rc;
+    if (list == object) return fail(RT_EINVAL, "cannot add a list to itself");
+    auto* l = dynamic_cast<Hittables*>(s->obj[list].get());
+    if (!l) return fail(RT_EHANDLE, "not a Hittables object");
+    l->add(s->take(object));
+    return RT_OK;
+}
+int32_t orc_bvh_new(rt_scene* s, int32_t list) {
+    if (!s) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(list)) != RT_OK) return rc;
+    auto* l = dynamic_cast<Hittables*>(s->obj[list].get());
+    if (!l) return fail(RT_EHANDLE, "not a Hittables object");
+    GUARD_BEGIN
+    auto owned = s->take(list);
+    auto objs = std::move(static_cast<Hittables*>(owned.get())->objects);
+    return s->add_obj(BVH::from_vec(std::move(objs)));
+    GUARD_END
+}
+int32_t orc_build_box(rt_scene* s, const double a[3], const double b[3], int32_t mat) {
+    if (!s || !a || !b) return fail(RT_EINVAL, "null");
+    if (!s->mat_ok(mat)) return fail(RT_EHANDLE, "unknown material");
+    GUARD_BEGIN
+    return s->add_obj(build_box(v3(a), v3(b), s->mat[mat]));
+    GUARD_END
+}
+int32_t orc_transform_new(rt_scene* s, int32_t object, const double* off, const double* q, const double* sc) {
+    if (!s) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(object)) != RT_OK) return rc;
+    Quaternion quat = q ? Quaternion{q[0], q[1], q[2], q[3]} : Quaternion::identity();
+    return s->add_obj(std::make_unique<Transform>(s->take(object), off ? v3(off) : Vec3(0, 0, 0), quat,
+                                                  sc ? v3(sc) : Vec3(1, 1, 1)));
+}
+int32_t orc_constant_medium_new(rt_scene* s, int32_t boundary, double density, int32_t tex) {
+    if (!s) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(boundary)) != RT_OK) return rc;
+    if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
+    return s->add_obj(std::make_unique<ConstantMedium>(s->take(boundary), density, s->tex[tex], s->next_medium_id++));
+}
+
+int32_t orc_quat_from_axis_angle(const double axis[3], double deg, double out[4]) {
+    GUARD_BEGIN
+    Quaternion q = Quaternion::from_axis_angle(v3(axis), deg);
+    out[0] = q.w;
+    out[1] = q.x;
+    out[2] = q.y;
+    out[3] = q.z;
+    return RT_OK;
+    GUARD_END
+}
+void orc_quat_from_euler(double yaw, double pitch, double roll, double out[4]) {
+    Quaternion q = Quaternion::from_euler(yaw, pitch, roll);
+    out[0] = q.w;
+    out[1] = q.x;
+    out[2] = q.y;
+    out[3] = q.z;
+}
+
+void orc_camera_default(rt_camera* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->aspect_ratio = 1.0;
+    c->image_width = 100;
+    c->samples_per_pixel = 10;
+    c->max_depth = 10;
+    c->background_tex = -1;
+    c->vertical_fov_in_degrees = 90.0;
+    c->look_at[2] = -1.0;
+    c->vec_up[1] = 1.0;
+    c->focus_distance = 10.0;
+}
+uint32_t orc_camera_image_height(const rt_camera* c) {
+    uint32_t h = (uint32_t)((double)c->image_width / c->aspect_ratio);
+    return h < 1 ? 1 : h;
+}
+void orc_render_opts_default(rt_render_opts* o) {
+    std::memset(o, 0, sizeof(*o));
+    o->seed = 1;
+    o->row_stride = 1;
+}
+uint32_t orc_shard_rows(const rt_camera* c, const rt_render_opts* o) {
+    uint32_t H = orc_camera_image_height(c);
+    uint32_t stride = (o && o->row_stride > 1) ? o->row_stride : 1;
+    uint32_t off = o ? o->row_offset : 0;
+    if (off >= H) return 0;
+    return (H - off + stride - 1) / stride;
+}
+
+// Oracle-only extras for tests and the CPU baseline: f64 output and the
+// instrumented work counts of SURVEY §8(d).
+int32_t orc_render_f64(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,
+                       double* out_linear, uint8_t* out_srgb, rt_stats* stats, uint64_t* work_counts,
+                       uint32_t row_begin, uint32_t row_end) {
+    if (!s || !c) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(world)) != RT_OK) return rc;
+    if (lights != -1 && (rc = s->check_obj(lights)) != RT_OK) return rc;
+    if (c->background_tex != -1 && !s->tex_ok(c->background_tex)) return fail(RT_EHANDLE, "unknown background");
+    if (c->image_width == 0 || !(c->aspect_ratio > 0)) return fail(RT_EINVAL, "bad image size");
+    GUARD_BEGIN
+    Camera cam;
+    cam.aspect_ratio = c->aspect_ratio;
+    cam.image_width = c->image_width;
+    cam.samples_per_pixel = c->samples_per_pixel;
+    cam.max_depth = c->max_depth;
+    cam.background = c->background_tex == -1 ? nullptr : s->tex[c->background_tex];
+    cam.vertical_fov_in_degrees = c->vertical_fov_in_degrees;
+    cam.look_from = v3(c->look_from);
+    cam.look_at = v3(c->look_at);
+    cam.vec_up = v3(c->vec_up);
+    cam.defocus_angle_in_degrees = c->defocus_angle_in_degrees;
+    cam.focus_distance = c->focus_distance;
+    cam.toon_map = c->toon_map == 1 ? ToonMap::ACES : ToonMap::None;
+    int threads = (o && o->threads) ? (int)o->threads : (int)std::thread::hardware_concurrency();
+    if (threads < 1) threads = 1;
+    std::vector<double> lin;
+    std::vector<uint8_t> srgb;
+    RenderResult res = render(cam, *s->obj[world], lights == -1 ? nullptr : s->obj[lights].get(), o ? o->seed : 1,
+                              threads, lin, out_srgb ? &srgb : nullptr, row_begin, row_end);
+    const uint32_t W = res.width;
+    for (uint32_t y = row_begin; y < std::min(row_end, res.height); ++y) {
+        size_t base = (size_t)y * W * 3;
+        if (out_linear) std::memcpy(out_linear + (size_t)(y - row_begin) * W * 3, &lin[base], (size_t)W * 3 * 8);
+        if (out_srgb) std::memcpy(out_srgb + (size_t)(y - row_begin) * W * 3, &srgb[base], (size_t)W * 3);
+    }
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        uint64_t rows = std::min(row_end, res.height) - std::min(row_begin, res.height);
+        stats->samples = rows * W * (uint64_t)cam.sqrt_spp * cam.sqrt_spp;
+        stats->rays = res.counts.ray_color_calls;
+        stats->render_ms = res.seconds * 1e3;
+    }
+    if (work_counts) std::memcpy(work_counts, &res.counts, sizeof(WorkCounts));
+    return RT_OK;
+    GUARD_END
+}
+uint32_t orc_work_count_fields(void) { return sizeof(WorkCounts) / sizeof(uint64_t); }
+
+int32_t orc_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,
+                   float* out_linear, uint8_t* out_srgb, rt_stats* stats) {
+    rt_render_opts def;
+    orc_render_opts_default(&def);
+    if (!o) o = &def;
+    uint32_t H = orc_camera_image_height(c), W = c->image_width;
+    uint32_t stride = o->row_stride > 1 ? o->row_stride : 1;
+    std::vector<double> lin((size_t)H * W * 3);
+    std::vector<uint8_t> srgb(out_srgb ? (size_t)H * W * 3 : 0);
+    int32_t rc = orc_render_f64(s, world, lights, c, o, lin.data(), out_srgb ? srgb.data() : nullptr, stats, nullptr,
+                                0, H);
+    if (rc != RT_OK) return rc;
+    uint32_t k = 0;
+    for (uint32_t y = o->row_offset; y < H; y += stride, ++k) {
+        for (size_t x = 0; x < (size_t)W * 3; ++x) {
+            if (out_linear) out_linear[(size_t)k * W * 3 + x] = (float)lin[(size_t)y * W * 3 + x];
+            if (out_srgb) out_srgb[(size_t)k * W * 3 + x] = srgb[(size_t)y * W * 3 + x];
+        }
+    }
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,29 @@
+"""raytracer-2025_amd -- MI355X (gfx950) render path for caidj0/Raytracer-2025.
+
+The product is librt_mi355x.so (HIP kernels + C ABI, include/rt_mi355x.h),
+built in-tree next to this file.  `load()` loads it and fails loudly if it is
+missing or was not built; there is no CPU fallback.
+"""
+import ctypes
+import os
+
+from .capi import Api, RtError  # noqa: F401
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librt_mi355x.so")
+
+_api = None
+
+
+def load():
+    """The gfx950 implementation of the ABI (prefix rt_)."""
+    global _api
+    if _api is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `make -C raytracer-2025_amd` or __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        api = Api(lib, "rt_")
+        if api.missing:
+            raise RuntimeError(f"{LIB_PATH} lacks symbols: {api.missing}")
+        _api = api
+    return _api
