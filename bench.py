@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s on the book-1 random-spheres scene at
+1920x1080, "512 spp" (= 22^2 = 484 traced strata, camera.rs:212), max_depth 50,
+f64 -- BASELINE.json configs[1] (C2) on 1..8 MI355X.
+
+A step renders one whole frame: every rank renders its interleaved rows
+(row_offset = rank, row_stride = N) with the gfx950 kernel through the C ABI
+(rt_render_device on torch's current stream), then the linear framebuffer is
+gathered to rank 0 over RCCL (N > 1).  Scaling is strong: the frame is fixed,
+ranks split it.  value = traced samples of all steps / max-over-ranks time.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PKG = "raytracer-2025_amd"
+
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec (half the 157.3 TF f32 vector rate)
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(threads, row_stride, spp):
+    """The TEST-ONLY oracle (reference algorithm, f64, recursive ray_color,
+    reference BVH topology) on the host cores: a bounded sample of the same
+    C2 workload -- every `row_stride`-th row of the 1920x1080 frame at `spp`
+    (sqrt_spp^2 strata).  Per-sample cost does not depend on spp."""
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    capi = importlib.import_module(PKG + ".capi")
+    rt = importlib.import_module(PKG + ".raytracer")
+    scenes = importlib.import_module(PKG + ".scenes")
+    api = capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
+    scene = rt.Scene(api)
+    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    c = cam.to_c()
+    opts = capi.RtRenderOpts()
+    api.render_opts_default(ctypes.byref(opts))
+    opts.seed = 1
+    opts.row_offset = 0
+    opts.row_stride = row_stride
+    opts.threads = threads
+    st = capi.RtStats()
+    t0 = time.perf_counter()
+    api.check(api.render_f64(scene.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts), None, None, ctypes.byref(st), None))
+    dt = time.perf_counter() - t0
+    return {
+        "value": st.samples / dt / 1e6,
+        "unit": "Msamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"C2 scene, every {row_stride}th row of 1920x1080 at {spp} spp ({cam.sqrt_spp**2} traced), "
+                  f"{st.samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
+                  "(oracle/: reference-semantics C++ restatement, not the Rust binary)",
+    }
+
+
+def load_pmc_traffic(path):
+    """HBM bytes per launch of the path kernel from a committed rocprofv3 PMC
+    summary (profiles/), or None."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-row-stride", type=int, default=2)
+    ap.add_argument("--cpu-spp", type=int, default=16)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        if world_size == 1 and args.gpus > 1:
+            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one process per GPU)",
+                  file=sys.stderr)
+            sys.exit(2)
+    distributed = world_size > 1
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if distributed:
+        dist.init_process_group("nccl", device_id=device)
+
+    pkg = importlib.import_module(PKG)
+    rt = importlib.import_module(PKG + ".raytracer")
+    scenes = importlib.import_module(PKG + ".scenes")
+    capi = importlib.import_module(PKG + ".capi")
+    pdist = importlib.import_module(PKG + ".dist")
+    api = pkg.load()
+
+    scene = rt.Scene(api)
+    world, lights, cam = scenes.random_spheres(scene, args.width, args.spp)
+    H, W = cam.image_height, cam.image_width
+    c = cam.to_c()
+    opts = capi.RtRenderOpts()
+    api.render_opts_default(ctypes.byref(opts))
+    opts.seed = args.seed
+    opts.row_offset = rank
+    opts.row_stride = world_size
+    rows = api.shard_rows(ctypes.byref(c), ctypes.byref(opts))
+    out = torch.empty((max(rows, 1), W, 3), dtype=torch.float32, device=device)
+    stream = torch.cuda.current_stream(device)
+    opts.stream = ctypes.c_void_p(stream.cuda_stream)
+    lights_h = -1 if lights is None else lights.h
+    kernel_ms = []
+
+    def step(record):
+        api.check(api.render_device(scene.s, world.h, lights_h, ctypes.byref(c), ctypes.byref(opts),
+                                    ctypes.c_void_p(out.data_ptr())))
+        st = capi.RtStats()
+        api.check(api.render_device_wait(scene.s, ctypes.byref(st)))  # HIP events around the path kernel
+        if record:
+            kernel_ms.append(st.kernel_ms)
+        frame = pdist.gather_frame(out[:rows], H, W) if distributed else out
+        return frame, st
+
+    for _ in range(args.warmup):
+        step(False)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame, st = step(True)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+        km = torch.tensor([sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device=device)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        kernel_avg_ms = km.item()
+    else:
+        kernel_avg_ms = sum(kernel_ms) / len(kernel_ms)
+
+    sqrt_spp = cam.sqrt_spp
+    frame_samples = W * H * sqrt_spp * sqrt_spp
+    value = frame_samples * args.steps / elapsed / 1e6
+    if rank == 0:
+        assert torch.isfinite(frame).all().item()
+        wc_path = os.path.join(ROOT, "bench_data", "work_counts_c2.json")
+        wc = json.load(open(wc_path))
+        # one launch of the path kernel processes this rank's rows
+        launch_samples = W * rows * sqrt_spp * sqrt_spp
+        flops = wc["flops_per_sample"] * launch_samples
+        achieved = flops / (kernel_avg_ms * 1e-3) / 1e12
+        traffic = load_pmc_traffic(os.path.join(ROOT, "profiles", "r01", "pmc_c2.json")) if world_size == 1 else None
+        line = {
+            "metric": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: book-1 random spheres from SplitMix64(2025) (raytracer-2025_amd/data), render RNG seed "
+                    + str(args.seed),
+            "config": {
+                "workload": f"C2: book-1 random spheres {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth 50, "
+                            "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
+                "frame_samples": frame_samples,
+                "parallelism": f"row-shard x{world_size}",
+            },
+            "roofline": {
+                "bound": "valu-fp64",
+                "achieved": round(achieved, 4),
+                "peak": FP64_VECTOR_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP64_VECTOR_PEAK_TFLOPS, 5),
+                "traffic": traffic,
+                "kernel": "rt_path_kernel",
+                "kernel_ms_avg": round(kernel_avg_ms, 3),
+                "flops_per_sample": round(wc["flops_per_sample"], 1),
+                "note": "algorithmic f64 FLOPs (reference algorithm on the reference BVH topology, "
+                        "bench_data/work_counts_c2.json) per launch / path-kernel time (HIP events on the render stream)",
+            },
+        }
+        if world_size == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, args.cpu_spp)
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

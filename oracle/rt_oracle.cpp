@@ -548,15 +548,15 @@ void to_rgb(const Color& c, ToonMap tm, uint8_t out[3]) {
 // camera.rs:161-202 -- rayon par_bridge over pixels restated as a dynamic
 // pixel-chunk queue over `threads` std::threads.
 RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, uint64_t seed, int threads,
-                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_begin, uint32_t row_end) {
+                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_offset, uint32_t row_stride) {
     cam.initialize();
     const uint32_t W = cam.image_width, H = cam.image_height;
-    if (row_end > H) row_end = H;
-    if (row_begin > row_end) row_begin = row_end;
-    linear.assign((size_t)W * H * 3, 0.0);
-    if (srgb) srgb->assign((size_t)W * H * 3, 0);
-    std::atomic<uint64_t> next{(uint64_t)row_begin * W};
-    const uint64_t end = (uint64_t)row_end * W;
+    if (row_stride < 1) row_stride = 1;
+    const uint32_t rows = row_offset >= H ? 0 : (H - row_offset + row_stride - 1) / row_stride;
+    linear.assign((size_t)W * rows * 3, 0.0);
+    if (srgb) srgb->assign((size_t)W * rows * 3, 0);
+    std::atomic<uint64_t> next{0};
+    const uint64_t end = (uint64_t)rows * W;
     std::vector<WorkCounts> per_thread(threads > 0 ? threads : 1);
     std::vector<std::string> errors(per_thread.size());
     auto t0 = std::chrono::steady_clock::now();
@@ -570,8 +570,9 @@ RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, 
                 uint64_t first = next.fetch_add(16);
                 if (first >= end) break;
                 uint64_t last = std::min<uint64_t>(first + 16, end);
-                for (uint64_t pix = first; pix < last; ++pix) {
-                    uint32_t i = (uint32_t)(pix % W), j = (uint32_t)(pix / W);
+                for (uint64_t k = first; k < last; ++k) {
+                    uint32_t i = (uint32_t)(k % W), j = row_offset + (uint32_t)(k / W) * row_stride;
+                    uint64_t pix = (uint64_t)j * W + i;
                     Color pixel_color;
                     for (uint32_t s_i = 0; s_i < cam.sqrt_spp; ++s_i)
                         for (uint32_t s_j = 0; s_j < cam.sqrt_spp; ++s_j) {
@@ -582,11 +583,11 @@ RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, 
                             pixel_color += cam.ray_color(r, cam.max_depth, world, lights);
                         }
                     Color pc = pixel_color * cam.pixel_sample_scale;
-                    double* dst = &linear[pix * 3];
+                    double* dst = &linear[k * 3];
                     dst[0] = pc[0];
                     dst[1] = pc[1];
                     dst[2] = pc[2];
-                    if (srgb) to_rgb(pc, cam.toon_map, &(*srgb)[pix * 3]);
+                    if (srgb) to_rgb(pc, cam.toon_map, &(*srgb)[k * 3]);
                 }
             }
         } catch (const std::exception& e) {
@@ -603,6 +604,7 @@ RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, 
     RenderResult res;
     res.width = W;
     res.height = H;
+    res.rows = rows;
     res.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     for (auto& w : per_thread) res.counts.add(w);
     for (auto& e : errors)

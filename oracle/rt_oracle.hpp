@@ -736,14 +736,15 @@ Color aces_tonemap(const Color& c);
 void to_rgb(const Color& c, ToonMap tm, uint8_t out[3]);
 
 // Renders the frame; linear (pixel_color * pixel_sample_scale) as f64 into
-// `linear` (W*H*3) and the u8 sRGB image into `srgb` (optional).
+// `linear` (rows*W*3) and the u8 sRGB image into `srgb` (optional).
 struct RenderResult {
-    uint32_t width = 0, height = 0;
+    uint32_t width = 0, height = 0, rows = 0;
     WorkCounts counts;
     double seconds = 0.0;
 };
+// Rows y = row_offset + k*row_stride only, written compact (k-th row at k).
 RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, uint64_t seed, int threads,
-                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_begin = 0,
-                    uint32_t row_end = 0xFFFFFFFFu);
+                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_offset = 0,
+                    uint32_t row_stride = 1);
 
 }  // namespace orc

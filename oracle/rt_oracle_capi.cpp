@@ -263,8 +263,7 @@ uint32_t orc_shard_rows(const rt_camera* c, const rt_render_opts* o) {
 // Oracle-only extras for tests and the CPU baseline: f64 output and the
 // instrumented work counts of SURVEY §8(d).
 int32_t orc_render_f64(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,
-                       double* out_linear, uint8_t* out_srgb, rt_stats* stats, uint64_t* work_counts,
-                       uint32_t row_begin, uint32_t row_end) {
+                       double* out_linear, uint8_t* out_srgb, rt_stats* stats, uint64_t* work_counts) {
     if (!s || !c) return fail(RT_EINVAL, "null");
     int32_t rc;
     if ((rc = s->check_obj(world)) != RT_OK) return rc;
@@ -290,17 +289,13 @@ int32_t orc_render_f64(rt_scene* s, int32_t world, int32_t lights, const rt_came
     std::vector<double> lin;
     std::vector<uint8_t> srgb;
     RenderResult res = render(cam, *s->obj[world], lights == -1 ? nullptr : s->obj[lights].get(), o ? o->seed : 1,
-                              threads, lin, out_srgb ? &srgb : nullptr, row_begin, row_end);
-    const uint32_t W = res.width;
-    for (uint32_t y = row_begin; y < std::min(row_end, res.height); ++y) {
-        size_t base = (size_t)y * W * 3;
-        if (out_linear) std::memcpy(out_linear + (size_t)(y - row_begin) * W * 3, &lin[base], (size_t)W * 3 * 8);
-        if (out_srgb) std::memcpy(out_srgb + (size_t)(y - row_begin) * W * 3, &srgb[base], (size_t)W * 3);
-    }
+                              threads, lin, out_srgb ? &srgb : nullptr, o ? o->row_offset : 0,
+                              (o && o->row_stride > 1) ? o->row_stride : 1);
+    if (out_linear && !lin.empty()) std::memcpy(out_linear, lin.data(), lin.size() * sizeof(double));
+    if (out_srgb && !srgb.empty()) std::memcpy(out_srgb, srgb.data(), srgb.size());
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
-        uint64_t rows = std::min(row_end, res.height) - std::min(row_begin, res.height);
-        stats->samples = rows * W * (uint64_t)cam.sqrt_spp * cam.sqrt_spp;
+        stats->samples = (uint64_t)res.rows * res.width * (uint64_t)cam.sqrt_spp * cam.sqrt_spp;
         stats->rays = res.counts.ray_color_calls;
         stats->render_ms = res.seconds * 1e3;
     }
@@ -312,23 +307,13 @@ uint32_t orc_work_count_fields(void) { return sizeof(WorkCounts) / sizeof(uint64
 
 int32_t orc_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,
                    float* out_linear, uint8_t* out_srgb, rt_stats* stats) {
-    rt_render_opts def;
-    orc_render_opts_default(&def);
-    if (!o) o = &def;
-    uint32_t H = orc_camera_image_height(c), W = c->image_width;
-    uint32_t stride = o->row_stride > 1 ? o->row_stride : 1;
-    std::vector<double> lin((size_t)H * W * 3);
-    std::vector<uint8_t> srgb(out_srgb ? (size_t)H * W * 3 : 0);
-    int32_t rc = orc_render_f64(s, world, lights, c, o, lin.data(), out_srgb ? srgb.data() : nullptr, stats, nullptr,
-                                0, H);
+    if (!c) return fail(RT_EINVAL, "null");
+    const size_t n = (size_t)orc_shard_rows(c, o) * c->image_width * 3;
+    std::vector<double> lin(n);
+    int32_t rc = orc_render_f64(s, world, lights, c, o, lin.data(), out_srgb, stats, nullptr);
     if (rc != RT_OK) return rc;
-    uint32_t k = 0;
-    for (uint32_t y = o->row_offset; y < H; y += stride, ++k) {
-        for (size_t x = 0; x < (size_t)W * 3; ++x) {
-            if (out_linear) out_linear[(size_t)k * W * 3 + x] = (float)lin[(size_t)y * W * 3 + x];
-            if (out_srgb) out_srgb[(size_t)k * W * 3 + x] = srgb[(size_t)y * W * 3 + x];
-        }
-    }
+    if (out_linear)
+        for (size_t i = 0; i < n; ++i) out_linear[i] = (float)lin[i];
     return RT_OK;
 }
 

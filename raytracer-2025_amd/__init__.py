@@ -19,6 +19,13 @@ def load():
     """The gfx950 implementation of the ABI (prefix rt_)."""
     global _api
     if _api is None:
+        # One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+        # libamdhip64.so.7).  Loading torch first makes librt_mi355x.so bind to
+        # that copy instead of pulling /opt/rocm's in beside it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run `make -C raytracer-2025_amd` or __graft_entry__.build()")
         lib = ctypes.CDLL(LIB_PATH)

@@ -105,7 +105,7 @@ SIGNATURES = {
 # Entry points only a CPU implementation has (the oracle).
 ORACLE_EXTRAS = {
     "render_f64": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _DP, C.POINTER(C.c_uint8),
-                        C.POINTER(RtStats), C.POINTER(C.c_uint64), _U, _U]),
+                        C.POINTER(RtStats), C.POINTER(C.c_uint64)]),
     "work_count_fields": (_U, []),
 }
 

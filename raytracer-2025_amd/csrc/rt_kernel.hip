@@ -1,0 +1,904 @@
+// rt_kernel.hip -- the persistent-threads f64 path-tracing megakernel for gfx950.
+//
+// One launch renders one frame (or one shard of rows) of Camera::render
+// (src/camera.rs:161-202).  Work item = (pixel, stratum row s_i): the lane
+// traces the sqrt_spp samples s_j of that row (camera.rs:183-192) one after
+// another and stores their f64 sum; rt_reduce sums the rows of a pixel in s_i
+// order and scales by pixel_sample_scale (camera.rs:193).
+//
+// ray_color's recursion (camera.rs:275-325) is run as a loop that carries a
+// path throughput `beta` and radiance `L`; a lane whose path ends starts the
+// next sample of its row at once, and a lane whose row ends takes the next row
+// from a device-wide counter.  Refills are aggregated per wave: __ballot of the
+// lanes that need work, one atomicAdd by the first of them, and each lane's
+// slot from its mbcnt rank -- the wave64 prefix-sum compaction that keeps all
+// 64 lanes tracing until the queue is empty.
+//
+// world.hit (hits.rs:34, bvh.rs:57, shapes.rs:88, volume.rs:37) is an explicit
+// depth-first walk over the flattened world (rt_layout.h) with a per-lane stack
+// in LDS, laid out [depth][lane] so a wave's pushes/pops hit 64 distinct banks.
+#include <hip/hip_runtime.h>
+
+#include "rt_kernel.h"
+#include "rt_math.h"
+
+namespace rtk {
+
+struct Ray {
+    D3 o, d;
+    double time;
+};
+
+struct Frame {
+    uint32_t W, rows, row_offset, row_stride;
+    uint32_t S;  // sqrt_spp
+    uint32_t max_depth;
+    uint32_t key0, key1;
+    uint32_t total_items;
+    uint32_t defocus;
+    double recip_sqrt_spp, pixel_sample_scale;
+    D3 center, pixel00, du, dv, disk_u, disk_v;
+};
+
+// ------------------------------------------------------------------ textures
+// texture.rs: SolidColor 33-36, CheckerTexture 60-73, ImageTexture 165-174,
+// NoiseTexture 191-196 (+ perlin.rs), book-1 sky.
+__device__ double perlin_noise(const DPerlin& P, D3 p) {
+    const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
+    const int64_t i = (int64_t)fx, j = (int64_t)fy, k = (int64_t)fz;
+    const double u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const double uu = u * u * (3.0 - 2.0 * u), vv = v * v * (3.0 - 2.0 * v), ww = w * w * (3.0 - 2.0 * w);
+    double accum = 0.0;
+    for (int di = 0; di < 2; ++di)
+        for (int dj = 0; dj < 2; ++dj)
+            for (int dk = 0; dk < 2; ++dk) {
+                const int idx = P.perm[0][(uint64_t)(i + di) & 255] ^ P.perm[1][(uint64_t)(j + dj) & 255] ^
+                                P.perm[2][(uint64_t)(k + dk) & 255];
+                const D3 c = d3(P.randvec[idx][0], P.randvec[idx][1], P.randvec[idx][2]);
+                const D3 wv = d3(u - di, v - dj, w - dk);
+                accum += (di * uu + (1 - di) * (1.0 - uu)) * (dj * vv + (1 - dj) * (1.0 - vv)) *
+                         (dk * ww + (1 - dk) * (1.0 - ww)) * dot(c, wv);
+            }
+    return accum;
+}
+
+__device__ void image_pixel(const SceneView& S, const DTexture& t, int64_t x, int64_t y, float out[4]) {
+    x = x < 0 ? 0 : (x > t.a - 1 ? t.a - 1 : x);
+    y = y < 0 ? 0 : (y > t.b - 1 ? t.b - 1 : y);
+    const float* px = S.texels + t.data + ((uint64_t)y * t.a + x) * 4;
+    out[0] = px[0];
+    out[1] = px[1];
+    out[2] = px[2];
+    out[3] = px[3];
+}
+
+__device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
+    for (int guard = 0; guard < 16; ++guard) {
+        const DTexture& t = S.textures[tid];
+        switch (t.type) {
+            case T_SOLID: return d3(t.color[0], t.color[1], t.color[2]);
+            case T_SKY: {
+                const double a = 0.5 * (p.y + 1.0);
+                return (1.0 - a) * d3(t.color[0], t.color[1], t.color[2]) + a * d3(t.color2[0], t.color2[1], t.color2[2]);
+            }
+            case T_CHECKER: {
+                const int32_t xi = (int32_t)floor(t.scale * p.x), yi = (int32_t)floor(t.scale * p.y),
+                              zi = (int32_t)floor(t.scale * p.z);
+                tid = ((xi + yi + zi) % 2 == 0) ? t.a : t.b;
+                continue;
+            }
+            case T_IMAGE: {
+                if (t.b == 0) return d3(0.0, 1.0, 1.0);  // texture.rs:167-169
+                const double uu = u - floor(u);
+                const double vv = 1.0 - (v - floor(v));
+                float px[4];
+                if (!t.c) {
+                    const uint32_t i = (uint32_t)(uu * (double)t.a), j = (uint32_t)(vv * (double)t.b);
+                    image_pixel(S, t, i, j, px);
+                } else {
+                    const double x = uu * (double)t.a - 0.5, y = vv * (double)t.b - 0.5;
+                    const uint32_t x0 = (uint32_t)fmax(floor(x), 0.0), y0 = (uint32_t)fmax(floor(y), 0.0);
+                    const uint32_t x1 = min(x0 + 1, (uint32_t)t.a - 1), y1 = min(y0 + 1, (uint32_t)t.b - 1);
+                    const float dx = (float)(x - (double)x0), dy = (float)(y - (double)y0);
+                    float p00[4], p10[4], p01[4], p11[4];
+                    image_pixel(S, t, x0, y0, p00);
+                    image_pixel(S, t, x1, y0, p10);
+                    image_pixel(S, t, x0, y1, p01);
+                    image_pixel(S, t, x1, y1, p11);
+                    for (int c = 0; c < 4; ++c) {
+                        const float v0 = p00[c] * (1.0f - dx) + p10[c] * dx;
+                        const float v1 = p01[c] * (1.0f - dx) + p11[c] * dx;
+                        px[c] = v0 * (1.0f - dy) + v1 * dy;
+                    }
+                }
+                return d3(px[0], px[1], px[2]);
+            }
+            case T_NOISE: {
+                const DPerlin& P = S.perlin[t.data];
+                double accum = 0.0, weight = 1.0;
+                D3 tp = p;
+                for (int o = 0; o < 7; ++o) {
+                    accum += weight * perlin_noise(P, tp);
+                    tp = 2.0 * tp;
+                    weight = 0.5 * weight;
+                }
+                const double turb = fabs(accum);
+                return (1.0 + sin(t.scale * p.z + 10.0 * turb)) * d3(0.5, 0.5, 0.5);
+            }
+            default: return d3(0.0, 0.0, 0.0);
+        }
+    }
+    return d3(0.0, 0.0, 0.0);
+}
+
+// ------------------------------------------------------------------ geometry tests
+// aabb.rs:62-78 slab test; inv = 1/d per axis computed once per ray (same value).
+__device__ __forceinline__ bool slab(const DNode& n, const Ray& r, D3 inv, double tmin, double tmax) {
+    double t0 = (n.lo[0] - r.o.x) * inv.x, t1 = (n.hi[0] - r.o.x) * inv.x;
+    double lo = fmax(tmin, fmin(t0, t1)), hi = fmin(tmax, fmax(t0, t1));
+    if (!(lo <= hi)) return false;
+    t0 = (n.lo[1] - r.o.y) * inv.y;
+    t1 = (n.hi[1] - r.o.y) * inv.y;
+    lo = fmax(lo, fmin(t0, t1));
+    hi = fmin(hi, fmax(t0, t1));
+    if (!(lo <= hi)) return false;
+    t0 = (n.lo[2] - r.o.z) * inv.z;
+    t1 = (n.hi[2] - r.o.z) * inv.z;
+    lo = fmax(lo, fmin(t0, t1));
+    hi = fmin(hi, fmax(t0, t1));
+    return lo <= hi;
+}
+
+// sphere.rs:77-96 -- t of the accepted root, or false
+__device__ __forceinline__ bool sphere_t(D3 c, double radius, const Ray& r, double a, double tmin, double tmax,
+                                         double& t) {
+    const D3 oc = c - r.o;
+    const double h = dot(r.d, oc);
+    const double cc = len2(oc) - radius * radius;
+    const double disc = h * h - a * cc;
+    if (disc < 0.0) return false;
+    const double sq = sqrt(disc);
+    double root = (h - sq) / a;
+    if (!(root >= tmin && root <= tmax)) {
+        root = (h + sq) / a;
+        if (!(root >= tmin && root <= tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
+// quad.rs:71-102 / triangle.rs:69-98
+__device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& r, double tmin, double tmax,
+                                         double& t) {
+    const D3 n = d3(P.f[0], P.f[1], P.f[2]);
+    const double denom = dot(n, r.d);
+    if (fabs(denom) < 1e-8) return false;
+    const double tt = (P.f[3] - dot(n, r.o)) / denom;
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    const D3 hv = (r.o + tt * r.d) - d3(P.f[4], P.f[5], P.f[6]);
+    const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
+    const double alpha = dot(w, cross(hv, v));
+    const double beta = dot(w, cross(u, hv));
+    if (!(alpha >= 0.0 && alpha <= 1.0 && beta >= 0.0 && beta <= 1.0)) return false;
+    if (tri) {
+        const double ab = alpha + beta;
+        if (!(ab >= 0.0 && ab <= 1.0)) return false;
+    }
+    t = tt;
+    return true;
+}
+
+// Transform::detransform (shapes.rs:80-84): R^-1 (v - offset) / scale
+__device__ __forceinline__ D3 xf_in(const DXform& X, D3 v) {
+    return mat3(X.rinv, v - d3(X.off[0], X.off[1], X.off[2])) / d3(X.scale[0], X.scale[1], X.scale[2]);
+}
+// Transform::transform (shapes.rs:74-78): R (v * scale) + offset
+__device__ __forceinline__ D3 xf_out(const DXform& X, D3 v) {
+    return mat3(X.rot, v * d3(X.scale[0], X.scale[1], X.scale[2])) + d3(X.off[0], X.off[1], X.off[2]);
+}
+// shapes.rs:93-99 local ray
+__device__ __forceinline__ Ray xf_ray(const DXform& X, const Ray& r) {
+    const D3 lo = xf_in(X, r.o);
+    const D3 lt = xf_in(X, r.o + 1.0 * r.d);
+    return Ray{lo, lt - lo, r.time};
+}
+__device__ __forceinline__ D3 inv_dir(D3 d) { return d3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z); }
+
+constexpr int MAX_XF = 2;
+
+struct HitInfo {
+    double t;
+    uint32_t ref;
+    uint32_t nxf;
+    uint32_t xf[MAX_XF];
+};
+
+// Closest t of a medium boundary (no media inside, no records).
+__device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax,
+                           uint32_t* stk, uint32_t sp0, double& tbest) {
+    Ray r = r0;
+    D3 inv = inv_dir(r.d);
+    double a = len2(r.d);
+    uint32_t xfs[MAX_XF];
+    uint32_t nxf = 0;
+    uint32_t sp = sp0;
+    uint32_t cur = root;
+    double c = tmax;
+    bool found = false;
+    for (;;) {
+        if (cur == REF_NONE) {
+            if (sp == sp0) break;
+            --sp;
+            cur = stk[sp * RT_BLOCK];
+        }
+        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+        cur = REF_NONE;
+        switch (kind) {
+            case K_BVH: {
+                const DNode n = S.nodes[idx];
+                if (slab(n, r, inv, tmin, c)) {
+                    if (n.right != REF_NONE) stk[(sp++) * RT_BLOCK] = n.right;
+                    cur = n.left;
+                }
+                break;
+            }
+            case K_LIST: {
+                const uint32_t child = S.list_children[idx];
+                if (child != REF_NONE) {
+                    if (S.list_children[idx + 1] != REF_NONE) stk[(sp++) * RT_BLOCK] = make_ref(K_LIST, idx + 1);
+                    cur = child;
+                }
+                break;
+            }
+            case K_SPHERE: {
+                const double4 s = S.spheres[idx];
+                double t;
+                if (sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t)) {
+                    c = t;
+                    found = true;
+                }
+                break;
+            }
+            case K_MSPHERE: {
+                const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
+                double t;
+                const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
+                if (sphere_t(cc, s.w, r, a, tmin, c, t)) {
+                    c = t;
+                    found = true;
+                }
+                break;
+            }
+            case K_QUAD:
+            case K_TRI: {
+                double t;
+                if (planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t)) {
+                    c = t;
+                    found = true;
+                }
+                break;
+            }
+            case K_XFORM: {
+                const DXform& X = S.xforms[idx];
+                stk[(sp++) * RT_BLOCK] = make_ref(K_POPXF, 0);
+                xfs[nxf++] = idx;
+                r = xf_ray(X, r);
+                inv = inv_dir(r.d);
+                a = len2(r.d);
+                cur = X.child;
+                break;
+            }
+            case K_POPXF: {
+                --nxf;
+                r = r0;
+                for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
+                inv = inv_dir(r.d);
+                a = len2(r.d);
+                break;
+            }
+            default: break;
+        }
+    }
+    tbest = c;
+    return found;
+}
+
+// world.hit(r, [1e-8, inf)) (camera.rs:286) as a DFS with one running closest
+// t: left subtree before right with the right interval shrunk (bvh.rs:70-82).
+__device__ bool trace(const SceneView& S, const Ray& wr, uint32_t* stk, const Rng& rng, HitInfo& hit) {
+    const double tmin = 1e-8;
+    Ray r = wr;
+    D3 inv = inv_dir(r.d);
+    double a = len2(r.d);
+    uint32_t xfs[MAX_XF];
+    uint32_t nxf = 0;
+    uint32_t sp = 0;
+    uint32_t cur = S.world_root;
+    double c = __builtin_huge_val();
+    bool found = false;
+    for (;;) {
+        if (cur == REF_NONE) {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * RT_BLOCK];
+        }
+        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+        const uint32_t this_ref = cur;
+        cur = REF_NONE;
+        double t;
+        bool got = false;
+        switch (kind) {
+            case K_BVH: {
+                const DNode n = S.nodes[idx];
+                if (slab(n, r, inv, tmin, c)) {
+                    if (n.right != REF_NONE) stk[(sp++) * RT_BLOCK] = n.right;
+                    cur = n.left;
+                }
+                break;
+            }
+            case K_LIST: {
+                const uint32_t child = S.list_children[idx];
+                if (child != REF_NONE) {
+                    if (S.list_children[idx + 1] != REF_NONE) stk[(sp++) * RT_BLOCK] = make_ref(K_LIST, idx + 1);
+                    cur = child;
+                }
+                break;
+            }
+            case K_SPHERE: {
+                const double4 s = S.spheres[idx];
+                got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t);
+                break;
+            }
+            case K_MSPHERE: {
+                const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
+                const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
+                got = sphere_t(cc, s.w, r, a, tmin, c, t);
+                break;
+            }
+            case K_QUAD:
+            case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t); break;
+            case K_XFORM: {
+                const DXform& X = S.xforms[idx];
+                stk[(sp++) * RT_BLOCK] = make_ref(K_POPXF, 0);
+                xfs[nxf++] = idx;
+                r = xf_ray(X, r);
+                inv = inv_dir(r.d);
+                a = len2(r.d);
+                cur = X.child;
+                break;
+            }
+            case K_POPXF: {
+                --nxf;
+                r = wr;
+                for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
+                inv = inv_dir(r.d);
+                a = len2(r.d);
+                break;
+            }
+            case K_MEDIUM: {
+                // volume.rs:37-73
+                const DMedium M = S.media[idx];
+                double t1, t2;
+                const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
+                if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, sp, t1)) break;
+                if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, sp, t2)) break;
+                if (t1 < tmin) t1 = tmin;
+                if (t2 > c) t2 = c;
+                if (t1 >= t2) break;
+                if (t1 < 0.0) t1 = 0.0;
+                const double ray_length = len(r.d);
+                const double inside = (t2 - t1) * ray_length;
+                const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
+                if (hd > inside) break;
+                t = t1 + hd / ray_length;  // volume.rs:65
+                got = true;
+                break;
+            }
+            default: break;
+        }
+        if (got && (t <= c)) {
+            c = t;
+            found = true;
+            hit.t = t;
+            hit.ref = this_ref;
+            hit.nxf = nxf;
+            for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
+        }
+    }
+    return found;
+}
+
+// ------------------------------------------------------------------ hit record
+struct Rec {
+    D3 p, n;
+    double u, v;
+    int mat;
+    bool front;
+};
+
+// HitRecord::new (hit.rs:24-43) of the recorded closest hit, in the frame of
+// its innermost Transform, then carried out through the chain (shapes.rs:104-108).
+__device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, bool need_uv_any) {
+    Ray r = wr;
+    for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf[k]], r);
+    const uint32_t kind = ref_kind(h.ref), idx = ref_index(h.ref);
+    Rec rec;
+    rec.u = 0.0;
+    rec.v = 0.0;
+    const D3 p = r.o + h.t * r.d;
+    D3 outward;
+    if (kind == K_SPHERE || kind == K_MSPHERE) {
+        D3 c;
+        double radius;
+        if (kind == K_SPHERE) {
+            const double4 s = S.spheres[idx];
+            c = d3(s.x, s.y, s.z);
+            radius = s.w;
+            rec.mat = S.sphere_mat[idx];
+        } else {
+            const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
+            c = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
+            radius = s.w;
+            rec.mat = S.msph_mat[idx];
+        }
+        outward = divs(p - c, radius);  // sphere.rs:99
+        if (need_uv_any && (S.materials[rec.mat].flags & MF_NEEDS_UV)) {
+            // sphere.rs:53-61
+            const double theta = acos(-outward.y);
+            const double phi = atan2(-outward.z, outward.x) + PI;
+            rec.u = phi / (2.0 * PI);
+            rec.v = theta / PI;
+        }
+    } else if (kind == K_QUAD || kind == K_TRI) {
+        const DPlanar& P = S.planars[idx];
+        outward = d3(P.f[0], P.f[1], P.f[2]);
+        const D3 hv = p - d3(P.f[4], P.f[5], P.f[6]);
+        const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
+        rec.u = dot(w, cross(hv, v));
+        rec.v = dot(w, cross(u, hv));
+        rec.mat = S.planar_mat[idx];
+    } else {  // K_MEDIUM (volume.rs:67-72)
+        outward = d3(1.0, 0.0, 0.0);
+        rec.mat = S.media[idx].phase_mat;
+    }
+    rec.front = dot(r.d, outward) < 0.0;
+    rec.n = rec.front ? outward : -outward;
+    rec.p = p;
+    for (int k = (int)h.nxf - 1; k >= 0; --k) {
+        const DXform& X = S.xforms[h.xf[k]];
+        rec.p = xf_out(X, rec.p);
+        bool ok;
+        rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
+    }
+    return rec;
+}
+
+// ------------------------------------------------------------------ lights (pdf.rs:66-88)
+__device__ double light_pdf_one(const SceneView& S, uint32_t ref, D3 o, D3 d) {
+    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    const Ray r{o, d, 0.0};
+    double t;
+    if (kind == K_QUAD || kind == K_TRI) {  // quad.rs:108-120
+        const DPlanar& P = S.planars[idx];
+        if (!planar_t(P, kind == K_TRI, r, 1e-8, __builtin_huge_val(), t)) return 0.0;
+        const D3 n = d3(P.f[0], P.f[1], P.f[2]);
+        const double front = dot(d, n) < 0.0 ? 1.0 : -1.0;
+        const D3 rn = front * n;
+        const double distance_squared = t * t * len2(d);
+        const double cosine = fabs(dot(d, rn) / len(d));
+        return distance_squared / (cosine * S.planar_area[idx]);
+    }
+    if (kind == K_SPHERE) {  // sphere.rs:114-132
+        const double4 s = S.spheres[idx];
+        if (!sphere_t(d3(s.x, s.y, s.z), s.w, r, len2(d), 1e-8, __builtin_huge_val(), t)) return 0.0;
+        const double dist_squared = len2(d3(s.x, s.y, s.z) - o);
+        const double ctm = sqrt(1.0 - s.w * s.w / dist_squared);
+        if (isnan(ctm)) return 1.0 / (4.0 * PI);
+        return 1.0 / (2.0 * PI * (1.0 - ctm));
+    }
+    return 0.0;
+}
+__device__ double light_pdf(const SceneView& S, D3 o, D3 d) {
+    const uint32_t root = S.lights_root;
+    if (ref_kind(root) != K_LIST) return light_pdf_one(S, root, o, d);
+    double sum = 0.0;  // hits.rs:52-67
+    uint32_t n = 0;
+    for (uint32_t i = ref_index(root); S.list_children[i] != REF_NONE; ++i, ++n) sum += light_pdf_one(S, S.list_children[i], o, d);
+    return sum / (double)n;
+}
+__device__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21, 34-38
+    const D3 a = fabs(n.x) > 0.9 ? d3(0.0, 1.0, 0.0) : d3(1.0, 0.0, 0.0);
+    const D3 u = unit(cross(n, a), ok);
+    const D3 w = cross(u, n);
+    return v.x * u + v.y * n + v.z * w;
+}
+__device__ D3 light_random(const SceneView& S, D3 o, Rng& rng, uint32_t& ovf, bool& ok) {
+    uint32_t ref = S.lights_root;
+    if (ref_kind(ref) == K_LIST) {  // hits.rs:69-75 choose
+        uint32_t n = 0;
+        for (uint32_t i = ref_index(ref); S.list_children[i] != REF_NONE; ++i) ++n;
+        uint32_t k = (uint32_t)(rng.next(ovf) * (double)n);
+        if (k >= n) k = n - 1;
+        ref = S.list_children[ref_index(ref) + k];
+    }
+    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    if (kind == K_QUAD || kind == K_TRI) {  // quad.rs:122-125, triangle.rs:117-128
+        const DPlanar& P = S.planars[idx];
+        double a = rng.next(ovf);
+        double b = rng.next(ovf);
+        if (kind == K_TRI && a + b > 1.0) {
+            const double na = 1.0 - b, nb = 1.0 - a;
+            a = na;
+            b = nb;
+        }
+        const D3 p = d3(P.f[4], P.f[5], P.f[6]) + (a * d3(P.f[7], P.f[8], P.f[9])) + (b * d3(P.f[10], P.f[11], P.f[12]));
+        return unit(p - o, ok);
+    }
+    // sphere.rs:134-144
+    const double4 s = S.spheres[idx];
+    const D3 direction = d3(s.x, s.y, s.z) - o;
+    const double distance_squared = len2(direction);
+    bool ok1, ok2;
+    const D3 nd = unit(direction, ok1);
+    const double r1 = rng.next(ovf), r2 = rng.next(ovf);
+    const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
+    const double phi = 2.0 * PI * r1;
+    const double x = cos(phi) * sqrt(1.0 - y * y), z = sin(phi) * sqrt(1.0 - y * y);
+    const D3 wv = onb_world(nd, d3(x, y, z), ok2);
+    bool ok3;
+    const D3 res = unit(wv, ok3);
+    ok = ok1 && ok2 && ok3;
+    return res;
+}
+
+// vec3.rs:313-322
+__device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
+    const double r1 = rng.next(ovf), r2 = rng.next(ovf);
+    double sn, cs;
+    sincos(2.0 * PI * r1, &sn, &cs);
+    const double s = sqrt(r2 * (1.0 - r2));
+    return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
+}
+
+// ------------------------------------------------------------------ the kernel
+struct LaneStats {
+    uint32_t rays, panics;
+};
+
+__global__ void __launch_bounds__(RT_BLOCK) rt_path_kernel(SceneView S, Frame F, uint32_t* __restrict__ queue,
+                                                          double* __restrict__ partial,
+                                                          unsigned long long* __restrict__ stats) {
+    __shared__ uint32_t stack_lds[RT_STACK * RT_BLOCK];
+    uint32_t* stk = stack_lds + threadIdx.x;
+    const uint32_t lane = __lane_id();
+
+    Rng rng;
+    rng.k0 = F.key0;
+    rng.k1 = F.key1;
+    uint32_t item = 0xFFFFFFFFu, s_j = 0, px = 0, py = 0;
+    bool need = true;
+    bool in_path = false;
+    Ray ray;
+    D3 beta = d3(1, 1, 1), L = d3(0, 0, 0), acc = d3(0, 0, 0);
+    uint32_t vertex = 0;
+    uint32_t n_rays = 0, n_panics = 0;
+
+    for (;;) {
+        // ---- refill: wave-aggregated dequeue of stratum rows
+        const unsigned long long mask = __ballot(need);
+        if (mask) {
+            const uint32_t leader = __ffsll((long long)mask) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(queue, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                item = base + rank;
+                if (item >= F.total_items) break;
+                need = false;
+                s_j = 0;
+                acc = d3(0, 0, 0);
+                const uint32_t pl = item / F.S;
+                px = pl % F.W;
+                py = F.row_offset + (pl / F.W) * F.row_stride;
+                rng.pixel = py * F.W + px;
+            }
+        }
+        if (!in_path) {
+            // ---- Camera::get_ray (camera.rs:247-273), vertex 0
+            const uint32_t s_i = item % F.S;
+            rng.sample = s_i * F.S + s_j;
+            rng.begin(0);
+            uint32_t ovf = 0;
+            const double xi0 = rng.next(ovf), xi1 = rng.next(ovf);
+            const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
+            const double oy = (((double)s_j + xi1) * F.recip_sqrt_spp) - 0.5;
+            const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
+            D3 origin = F.center;
+            if (F.defocus) {
+                const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
+                const double rr = sqrt(rng.next(ovf));
+                double sn, cs;
+                sincos(theta, &sn, &cs);
+                origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
+            }
+            ray.o = origin;
+            ray.d = ps - origin;
+            ray.time = rng.next(ovf);
+            beta = d3(1, 1, 1);
+            L = d3(0, 0, 0);
+            vertex = 1;
+            in_path = true;
+        }
+
+        // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
+        bool end_path = false;
+        uint32_t ovf = 0;
+        bool panic = false;
+        rng.begin(vertex);
+        ++n_rays;
+        HitInfo h;
+        if (!trace(S, ray, stk, rng, h)) {
+            // miss: Environment::value (environment.rs:14-24)
+            if (S.background_tex >= 0) {
+                bool ok;
+                const D3 p = unit(ray.d, ok);
+                if (!ok) panic = true;
+                double u = 0.0, v = 0.0;
+                if (S.textures[S.background_tex].needs_uv) {
+                    const double theta = acos(-p.y);
+                    const double phi = PI - atan2(-p.z, p.x);
+                    u = phi / (2.0 * PI);
+                    v = theta / PI;
+                }
+                L = L + beta * tex_value(S, S.background_tex, u, v, p);
+            }
+            end_path = true;
+        } else {
+            const Rec rec = make_record(S, ray, h, true);
+            int mat = rec.mat;
+            DMaterial M = S.materials[mat];
+            // emitted (material.rs:30-33, 171-178, 262-266)
+            if (M.flags & MF_EMISSIVE) {
+                D3 em;
+                if (M.type == M_DIFFUSE_LIGHT) {
+                    em = tex_value(S, M.tex, rec.u, rec.v, rec.p);
+                    D3 inner = d3(0, 0, 0);
+                    if (M.inner >= 0 && S.materials[M.inner].type == M_DIFFUSE_LIGHT) {
+                        const DMaterial& I = S.materials[M.inner];
+                        inner = tex_value(S, I.tex, rec.u, rec.v, rec.p);
+                    }
+                    em = em + inner;
+                } else {  // Mix
+                    const DMaterial& A = S.materials[M.inner];
+                    const DMaterial& B = S.materials[M.inner2];
+                    const D3 ea = A.type == M_DIFFUSE_LIGHT ? tex_value(S, A.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                    const D3 eb = B.type == M_DIFFUSE_LIGHT ? tex_value(S, B.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                    em = ((1.0 - M.fuzz) * ea) + (M.fuzz * eb);
+                }
+                L = L + beta * em;
+            }
+            // resolve wrappers: DiffuseLight(inner) scatters as inner; Mix draws (material.rs:254-260)
+            if (M.type == M_DIFFUSE_LIGHT) {
+                if (M.inner < 0) {
+                    end_path = true;
+                } else {
+                    mat = M.inner;
+                    M = S.materials[mat];
+                }
+            }
+            if (!end_path && M.type == M_MIX) {
+                mat = rng.next(ovf) > M.fuzz ? M.inner : M.inner2;
+                M = S.materials[mat];
+                if (M.type == M_DIFFUSE_LIGHT) end_path = true;  // DiffuseLight without inner: None
+            }
+            if (!end_path) {
+                const D3 n = rec.n;
+                int pdf_kind = -1;  // 0 cosine, 1 sphere
+                D3 albedo;
+                switch (M.type) {
+                    case M_LAMBERTIAN:  // material.rs:60-65
+                        albedo = tex_value(S, M.tex, rec.u, rec.v, rec.p);
+                        pdf_kind = 0;
+                        break;
+                    case M_EMPTY:  // material.rs:41-46
+                        albedo = d3(0.75, 0.75, 0.75);
+                        pdf_kind = 0;
+                        break;
+                    case M_ISOTROPIC:  // material.rs:199-206
+                        albedo = tex_value(S, M.tex, rec.u, rec.v, rec.p);
+                        pdf_kind = 1;
+                        break;
+                    case M_METAL: {  // material.rs:82-95
+                        bool ok1, ok2;
+                        const D3 ud = unit(ray.d, ok1);
+                        if (!ok1) {
+                            end_path = true;
+                            break;
+                        }
+                        const D3 rr = unit(reflect(ud, n), ok2);
+                        if (!ok2) {
+                            end_path = true;
+                            break;
+                        }
+                        const D3 ruv = random_unit_vector(rng, ovf);
+                        const D3 dir = rr + (M.fuzz * ruv);
+                        beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
+                        ray = Ray{rec.p, dir, ray.time};
+                        break;
+                    }
+                    case M_DIELECTRIC: {  // material.rs:117-143
+                        const double ri = rec.front ? 1.0 / M.fuzz : M.fuzz;
+                        bool ok;
+                        const D3 ud = unit(ray.d, ok);
+                        if (!ok) panic = true;
+                        const double cos_theta = fmin(dot(-ud, n), 1.0);
+                        const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+                        const bool cannot_refract = ri * sin_theta > 1.0;
+                        bool do_reflect = cannot_refract;
+                        if (!do_reflect) {
+                            const double r0 = (1.0 - ri) / (1.0 + ri);
+                            const double r0sq = r0 * r0;
+                            const double x = 1.0 - cos_theta;
+                            const double x2 = x * x;
+                            const double refl = r0sq + (1.0 - r0sq) * (x * (x2 * x2));
+                            do_reflect = refl > rng.next(ovf);
+                        }
+                        D3 dir;
+                        if (do_reflect) {
+                            dir = reflect(ud, n);
+                        } else {  // vec3.rs:345-354
+                            const double ct = fmin(dot(-ud, n), 1.0);
+                            const D3 perp = ri * (ud + ct * n);
+                            const double pl = sqrt(1.0 - len2(perp));
+                            if (isnan(pl)) panic = true;
+                            dir = perp + (-pl * n);
+                        }
+                        beta = beta * tex_value(S, M.tex, rec.u, rec.v, rec.p);
+                        ray = Ray{rec.p, dir, ray.time};
+                        break;
+                    }
+                    case M_TRANSPARENT:  // material.rs:211-217
+                        ray = Ray{rec.p, ray.d, ray.time};
+                        break;
+                    default: end_path = true; break;
+                }
+                if (pdf_kind >= 0 && !end_path) {
+                    // PDF branch (camera.rs:297-316)
+                    const bool use_lights = S.lights_root != REF_NONE;
+                    bool from_material = true;
+                    if (use_lights) from_material = rng.next(ovf) < 0.5;  // MixturePDF::generate (pdf.rs:113-119)
+                    D3 dir;
+                    bool ok = true;
+                    if (from_material) {
+                        if (pdf_kind == 0) {  // CosinePDF::generate (pdf.rs:59-63), vec3.rs:333-343
+                            const double r1 = rng.next(ovf), r2 = rng.next(ovf);
+                            const double phi = 2.0 * PI * r1;
+                            double sn, cs;
+                            sincos(phi, &sn, &cs);
+                            const double sr2 = sqrt(r2);
+                            dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
+                        } else {
+                            dir = random_unit_vector(rng, ovf);
+                        }
+                    } else {
+                        dir = light_random(S, rec.p, rng, ovf, ok);
+                    }
+                    if (!ok) panic = true;
+                    // value (pdf.rs:22-28, 50-57, 101-111)
+                    D3 f;
+                    double pdf0;
+                    if (pdf_kind == 0) {
+                        bool okd;
+                        const D3 ud = unit(dir, okd);
+                        if (!okd) panic = true;
+                        const double ct = dot(ud, n);
+                        pdf0 = fmax(0.0, ct / PI);
+                        f = divs(albedo * d3(fmax(ct, 0.0), fmax(ct, 0.0), fmax(ct, 0.0)), PI);
+                    } else {
+                        pdf0 = 1.0 / (4.0 * PI);
+                        f = divs(albedo, 4.0 * PI);
+                    }
+                    double pdf = pdf0;
+                    if (use_lights) {
+                        const double pdf1 = light_pdf(S, rec.p, dir);
+                        if (isnan(pdf1)) panic = true;
+                        if (pdf0 == 0.0 && pdf1 == 0.0) panic = true;
+                        pdf = pdf0 * 0.5 + pdf1 * 0.5;
+                    }
+                    if (pdf == 0.0) panic = true;  // camera.rs:309
+                    beta = beta * divs(f, pdf);
+                    ray = Ray{rec.p, dir, ray.time};
+                }
+            }
+        }
+        if (ovf) panic = true;
+        if (panic) {
+            ++n_panics;
+            end_path = true;
+        }
+        if (!end_path) {
+            ++vertex;
+            if (vertex > F.max_depth) end_path = true;  // depth == 0 -> BLACK (camera.rs:282-284)
+        }
+        if (end_path) {
+            if (isnan(L.x) || isnan(L.y) || isnan(L.z)) {  // camera.rs:323
+                ++n_panics;
+                L = d3(0, 0, 0);
+            }
+            acc = acc + L;
+            in_path = false;
+            ++s_j;
+            if (s_j == F.S) {
+                double* dst = partial + (uint64_t)item * 3;
+                dst[0] = acc.x;
+                dst[1] = acc.y;
+                dst[2] = acc.z;
+                need = true;
+            }
+        }
+    }
+    atomicAdd(&stats[0], (unsigned long long)n_rays);
+    if (n_panics) atomicAdd(&stats[1], (unsigned long long)n_panics);
+}
+
+// Sums the S stratum rows of each pixel in s_i order, * pixel_sample_scale,
+// to linear f32 (camera.rs:193) and optionally sRGB u8 (utils/color.rs:27-36).
+__global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
+                                                       double scale, float* __restrict__ out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    const double* src = partial + (uint64_t)p * S * 3;
+    double r = 0.0, g = 0.0, b = 0.0;
+    for (uint32_t k = 0; k < S; ++k) {
+        r += src[k * 3 + 0];
+        g += src[k * 3 + 1];
+        b += src[k * 3 + 2];
+    }
+    out[(uint64_t)p * 3 + 0] = (float)(r * scale);
+    out[(uint64_t)p * 3 + 1] = (float)(g * scale);
+    out[(uint64_t)p * 3 + 2] = (float)(b * scale);
+}
+
+}  // namespace rtk
+
+// ------------------------------------------------------------------ host launchers
+extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
+                                       double* partial, unsigned long long* stats, float* out, hipStream_t stream,
+                                       int grid) {
+    rtk::Frame F;
+    F.W = fd->W;
+    F.rows = fd->rows;
+    F.row_offset = fd->row_offset;
+    F.row_stride = fd->row_stride;
+    F.S = fd->S;
+    F.max_depth = fd->max_depth;
+    F.key0 = (uint32_t)fd->seed;
+    F.key1 = (uint32_t)(fd->seed >> 32);
+    F.total_items = fd->W * fd->rows * fd->S;
+    F.defocus = fd->defocus;
+    F.recip_sqrt_spp = fd->recip_sqrt_spp;
+    F.pixel_sample_scale = fd->pixel_sample_scale;
+    F.center = rtk::D3{fd->center[0], fd->center[1], fd->center[2]};
+    F.pixel00 = rtk::D3{fd->pixel00[0], fd->pixel00[1], fd->pixel00[2]};
+    F.du = rtk::D3{fd->du[0], fd->du[1], fd->du[2]};
+    F.dv = rtk::D3{fd->dv[0], fd->dv[1], fd->dv[2]};
+    F.disk_u = rtk::D3{fd->disk_u[0], fd->disk_u[1], fd->disk_u[2]};
+    F.disk_v = rtk::D3{fd->disk_v[0], fd->disk_v[1], fd->disk_v[2]};
+    hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    if (fd->ev_start) hipEventRecord((hipEvent_t)fd->ev_start, stream);
+    hipLaunchKernelGGL(rtk::rt_path_kernel, dim3(grid), dim3(RT_BLOCK), 0, stream, *view, F, queue, partial, stats);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (fd->ev_stop) hipEventRecord((hipEvent_t)fd->ev_stop, stream);
+    const uint32_t npix = fd->W * fd->rows;
+    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
+                       fd->pixel_sample_scale, out);
+    return hipGetLastError();
+}
+
+extern "C" int rtk_path_kernel_occupancy(int* blocks_per_cu) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel, RT_BLOCK, 0);
+}

@@ -1,0 +1,149 @@
+// rt_layout.h -- the flattened world as it lives in HBM.
+//
+// The reference world is a tree of Box<dyn Hittable> (src/hit.rs:46) walked by
+// recursive virtual calls (Hittables::hit hits.rs:34, BVH::hit bvh.rs:57,
+// Transform::hit shapes.rs:88, ConstantMedium::hit volume.rs:37).  Here it is
+// one read-only blob of typed arrays, and every edge of the tree is a 32-bit
+// `ref` = kind (top 4 bits) | index (low 28 bits), walked by an explicit
+// per-lane stack (rt_kernel.hip).
+//
+// Layout choices (DESIGN.md "Data layout in HBM"):
+//  - a BVH node is one 64-B record (AABB + both child refs): a traversal step
+//    of one lane is one 64-B line, i.e. 4 dwordx4 loads, never six scattered
+//    SoA streams (rays are incoherent after the first bounce);
+//  - hot geometry is split from cold attributes: spheres are a double4
+//    {center, radius} stream with materials in a separate int stream (read
+//    only for the closest hit); planar primitives keep the 16 doubles the hit
+//    test reads in one 128-B record and area/material apart;
+//  - materials/textures are small tables read once per bounce.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtk {
+
+enum RefKind : uint32_t {
+    K_NONE = 0,
+    K_BVH = 1,
+    K_LIST = 2,      // index = position in list_children (iterator form)
+    K_SPHERE = 3,
+    K_MSPHERE = 4,   // moving sphere (Sphere::new_with_motion)
+    K_QUAD = 5,
+    K_TRI = 6,
+    K_XFORM = 7,
+    K_MEDIUM = 8,
+    K_POPXF = 9,     // traversal-stack marker: leave a Transform's frame
+};
+
+__host__ __device__ inline uint32_t make_ref(uint32_t kind, uint32_t index) { return (kind << 28) | index; }
+__host__ __device__ inline uint32_t ref_kind(uint32_t r) { return r >> 28; }
+__host__ __device__ inline uint32_t ref_index(uint32_t r) { return r & 0x0FFFFFFFu; }
+constexpr uint32_t REF_NONE = 0u;
+
+// bvh.rs:5-9 -- AABB (aabb.rs:10-14) + left/right.  64 B.
+struct alignas(16) DNode {
+    double lo[3];
+    double hi[3];
+    uint32_t left, right;  // right may be REF_NONE (bvh.rs:25)
+};
+
+// Planar: quad.rs:17-27 / triangle.rs:16-26 hot fields, packed in 128 B:
+// f[0..3) unit normal, f[3] parm_d, f[4..7) anchor, f[7..10) u, f[10..13) v,
+// f[13..16) w = n / |n|^2.
+struct alignas(16) DPlanar {
+    double f[16];
+};
+
+// Transform (shapes.rs:23-29).  Rotation kept as the quaternion the reference
+// uses plus its 3x3 matrix form (the kernel rotates with the matrix).
+struct alignas(16) DXform {
+    double off[3];
+    double scale[3];
+    double rot[9];   // R(q), row-major
+    double rinv[9];  // R(conj q)
+    uint32_t child, pad;
+};
+
+// ConstantMedium (volume.rs:16-20)
+struct alignas(16) DMedium {
+    double neg_inv_density;
+    uint32_t boundary;
+    int32_t phase_mat;
+    uint32_t medium_id;
+    uint32_t pad;
+};
+
+enum MatType : int32_t {
+    M_LAMBERTIAN = 0,
+    M_METAL = 1,
+    M_DIELECTRIC = 2,
+    M_DIFFUSE_LIGHT = 3,
+    M_ISOTROPIC = 4,
+    M_EMPTY = 5,
+    M_TRANSPARENT = 6,
+    M_MIX = 7,
+};
+
+// material.rs: one record per Arc<dyn Material>
+struct alignas(16) DMaterial {
+    int32_t type;
+    int32_t tex;       // albedo / attenuation / emission texture
+    int32_t inner;     // DiffuseLight inner material, Mix mat1
+    int32_t inner2;    // Mix mat2
+    double albedo[3];  // Metal albedo
+    double fuzz;       // Metal fuzz (clamped), Dielectric ior, Mix ratio
+    uint32_t flags;    // MF_*
+    uint32_t pad[3];
+};
+enum : uint32_t { MF_NEEDS_UV = 1u, MF_EMISSIVE = 2u };
+
+enum TexType : int32_t {
+    T_SOLID = 0,
+    T_CHECKER = 1,
+    T_IMAGE = 2,
+    T_NOISE = 3,
+    T_SKY = 4,
+};
+
+struct alignas(16) DTexture {
+    int32_t type;
+    int32_t a, b;        // checker even/odd; image width/height
+    int32_t c;           // image linear-interp flag
+    double color[3];     // solid / sky horizon
+    double color2[3];    // sky zenith
+    double scale;        // checker inv_scale; noise scale
+    uint64_t data;       // image: float offset into texels; noise: index into perlin tables
+    uint32_t needs_uv, pad;
+};
+
+// perlin.rs:8-13
+struct alignas(16) DPerlin {
+    double randvec[256][3];
+    int32_t perm[3][256];
+};
+
+// Everything the kernel reads about the world, as device pointers.
+struct SceneView {
+    const DNode* nodes;
+    const double4* spheres;        // {cx, cy, cz, r}
+    const int32_t* sphere_mat;
+    const double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}
+    const double4* msph_dir;       // {c2-c1, 0}
+    const int32_t* msph_mat;
+    const DPlanar* planars;        // quads then triangles share the record
+    const double* planar_area;
+    const int32_t* planar_mat;
+    const uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
+    const DXform* xforms;
+    const DMedium* media;
+    const DMaterial* materials;
+    const DTexture* textures;
+    const float* texels;
+    const DPerlin* perlin;
+    uint32_t world_root;
+    uint32_t lights_root;  // REF_NONE = lights: None
+    int32_t background_tex;  // -1 = black
+    uint32_t stack_need;     // max traversal stack entries (host-computed)
+};
+
+}  // namespace rtk

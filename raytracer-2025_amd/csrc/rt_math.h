@@ -1,0 +1,107 @@
+// rt_math.h -- f64 vector math and the render RNG for the gfx950 kernel.
+//
+// Arithmetic follows the reference's expression order (src/utils/vec3.rs):
+// Div<f64> multiplies by the reciprocal (vec3.rs:226-232), dot/cross/length
+// as written there.  The RNG is the contract of oracle/rng_contract.hpp,
+// restated here for the device (Philox4x32-10, Random123 constants).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtk {
+
+constexpr double PI = 3.14159265358979323846264338327950288;
+
+struct D3 {
+    double x, y, z;
+};
+__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 operator+(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ D3 operator-(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ D3 operator*(D3 a, D3 b) { return d3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ D3 operator*(double s, D3 v) { return d3(s * v.x, s * v.y, s * v.z); }
+__device__ __forceinline__ D3 operator-(D3 a) { return d3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ D3 operator/(D3 a, D3 b) { return d3(a.x / b.x, a.y / b.y, a.z / b.z); }
+__device__ __forceinline__ D3 divs(D3 v, double s) { return (1.0 / s) * v; }
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ D3 cross(D3 a, D3 b) {
+    return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double len2(D3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ double len(D3 a) { return sqrt(len2(a)); }
+__device__ __forceinline__ bool finite3(D3 v) { return isfinite(v.x) && isfinite(v.y) && isfinite(v.z); }
+// UnitVec3::from_vec3 (vec3.rs:299-306): v / |v|, ok = all finite
+__device__ __forceinline__ D3 unit(D3 v, bool& ok) {
+    D3 u = divs(v, len(v));
+    ok = finite3(u);
+    return u;
+}
+// vec3.rs:71-73
+__device__ __forceinline__ D3 reflect(D3 v, D3 n) { return v - (2.0 * dot(v, n)) * n; }
+__device__ __forceinline__ D3 mat3(const double* m, D3 v) {
+    return d3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
+              m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+
+// ---------------------------------------------------------------- RNG
+__device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                              uint32_t k1) {
+#pragma unroll
+    for (int round = 0; round < 10; ++round) {
+        if (round > 0) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0;
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0;
+        const uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+}
+__device__ __forceinline__ double u64_unit(uint32_t lo, uint32_t hi) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    return (double)(v >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Keyed per-path stream (oracle/rng_contract.hpp): draw `slot` of path vertex
+// `vertex` of sample (pixel, sample).  Draws of one vertex come in pairs from
+// one Philox block; the odd half is cached.
+struct Rng {
+    uint32_t k0, k1, pixel, sample, vertex, slot;
+    uint32_t c_lo, c_hi;
+    __device__ __forceinline__ void begin(uint32_t v) {
+        vertex = v;
+        slot = 0;
+    }
+    __device__ __forceinline__ double next(uint32_t& overflow) {
+        if (slot >= 16u) {
+            overflow = 1;
+            slot = 0;
+        }
+        double r;
+        if ((slot & 1u) == 0u) {
+            uint32_t c0 = vertex * 8u + (slot >> 1), c1 = pixel, c2 = sample, c3 = 0u;
+            philox4x32_10(c0, c1, c2, c3, k0, k1);
+            c_lo = c2;
+            c_hi = c3;
+            r = u64_unit(c0, c1);
+        } else {
+            r = u64_unit(c_lo, c_hi);
+        }
+        ++slot;
+        return r;
+    }
+    __device__ __forceinline__ double medium(uint32_t id) const {
+        uint32_t c0 = vertex, c1 = pixel, c2 = sample, c3 = 1u + id;
+        philox4x32_10(c0, c1, c2, c3, k0, k1);
+        return u64_unit(c0, c1);
+    }
+};
+
+}  // namespace rtk

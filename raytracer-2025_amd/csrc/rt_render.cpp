@@ -1,0 +1,339 @@
+// rt_render.cpp -- render half of the C ABI: Camera::initilize on the host,
+// world upload (one device blob per scene, cached until the scene changes),
+// and the blocking / stream-ordered render entry points.
+#include <chrono>
+#include <cstring>
+#include <mutex>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_kernel.h"
+#include "rt_scene.hpp"
+
+namespace rth {
+
+struct DeviceWorld {
+    int device = -1;
+    int32_t world = -1, lights = -1, background = -1;
+    uint64_t generation = ~0ull;
+    char* blob = nullptr;
+    size_t blob_bytes = 0;
+    rtk::SceneView view{};
+    size_t n_prims = 0;
+    // frame work buffers (grow-only)
+    uint32_t* queue = nullptr;
+    unsigned long long* stats = nullptr;
+    double* partial = nullptr;
+    size_t partial_bytes = 0;
+    float* out = nullptr;
+    size_t out_bytes = 0;
+    hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+    // last async render
+    bool pending = false;
+    uint64_t pending_samples = 0;
+    double pending_flatten_ms = 0;
+    std::chrono::steady_clock::time_point pending_t0;
+    int grid = 0;
+    hipStream_t pending_stream = nullptr;
+};
+
+void destroy_device_world(DeviceWorld* d) {
+    if (!d) return;
+    if (d->blob) (void)hipFree(d->blob);
+    if (d->queue) (void)hipFree(d->queue);
+    if (d->stats) (void)hipFree(d->stats);
+    if (d->partial) (void)hipFree(d->partial);
+    if (d->out) (void)hipFree(d->out);
+    if (d->ev_start) (void)hipEventDestroy(d->ev_start);
+    if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
+    delete d;
+}
+
+static int32_t hip_fail(hipError_t e, const char* what) {
+    return set_error(RT_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+static size_t put(std::vector<char>& blob, const std::vector<T>& v) {
+    size_t off = (blob.size() + 255) & ~(size_t)255;
+    blob.resize(off + v.size() * sizeof(T));
+    if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+// Checks there is a gfx950 device and binds the scene's device world to it,
+// flattening + uploading when (world, lights, background, scene) changed.
+static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, double& flatten_ms) {
+    flatten_ms = 0;
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice (no HIP device)");
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(RT_EDEVICE, std::string("librt_mi355x.so needs a gfx950 device, found ") + prop.gcnArchName);
+    DeviceWorld* d = s->dev;
+    if (d && d->device != dev) {
+        destroy_device_world(d);
+        s->dev = d = nullptr;
+    }
+    if (!d) {
+        d = new DeviceWorld();
+        d->device = dev;
+        s->dev = d;
+        if ((e = hipMalloc(&d->queue, 256)) != hipSuccess) return hip_fail(e, "hipMalloc queue");
+        if ((e = hipMalloc(&d->stats, 256)) != hipSuccess) return hip_fail(e, "hipMalloc stats");
+        if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+        if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+        int bpc = 0;
+        if ((e = (hipError_t)rtk_path_kernel_occupancy(&bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
+        if (bpc < 1) bpc = 1;
+        d->grid = bpc * prop.multiProcessorCount;
+    }
+    if (d->blob && d->world == world && d->lights == lights && d->background == bg && d->generation == s->generation)
+        return RT_OK;
+    auto t0 = std::chrono::steady_clock::now();
+    HostWorld hw;
+    int32_t rc = flatten(s, world, lights, bg, hw);
+    if (rc != RT_OK) return rc;
+    if (hw.stack_need > RT_STACK)
+        return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
+                                        std::to_string(RT_STACK));
+    std::vector<char> blob;
+    size_t o_nodes = put(blob, hw.nodes), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
+           o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
+           o_pl = put(blob, hw.planars), o_pla = put(blob, hw.planar_area), o_plm = put(blob, hw.planar_mat),
+           o_lc = put(blob, hw.list_children), o_xf = put(blob, hw.xforms), o_md = put(blob, hw.media),
+           o_mat = put(blob, hw.materials), o_tex = put(blob, hw.textures), o_tx = put(blob, hw.texels),
+           o_per = put(blob, hw.perlin);
+    if (d->blob) {
+        (void)hipFree(d->blob);
+        d->blob = nullptr;
+    }
+    if ((e = hipMalloc(&d->blob, blob.size() + 256)) != hipSuccess) return hip_fail(e, "hipMalloc world");
+    if ((e = hipMemcpy(d->blob, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy world");
+    char* b = d->blob;
+    rtk::SceneView& v = d->view;
+    v.nodes = (const rtk::DNode*)(b + o_nodes);
+    v.spheres = (const double4*)(b + o_sph);
+    v.sphere_mat = (const int32_t*)(b + o_sphm);
+    v.msph_center = (const double4*)(b + o_msc);
+    v.msph_dir = (const double4*)(b + o_msd);
+    v.msph_mat = (const int32_t*)(b + o_msm);
+    v.planars = (const rtk::DPlanar*)(b + o_pl);
+    v.planar_area = (const double*)(b + o_pla);
+    v.planar_mat = (const int32_t*)(b + o_plm);
+    v.list_children = (const uint32_t*)(b + o_lc);
+    v.xforms = (const rtk::DXform*)(b + o_xf);
+    v.media = (const rtk::DMedium*)(b + o_md);
+    v.materials = (const rtk::DMaterial*)(b + o_mat);
+    v.textures = (const rtk::DTexture*)(b + o_tex);
+    v.texels = (const float*)(b + o_tx);
+    v.perlin = (const rtk::DPerlin*)(b + o_per);
+    v.world_root = hw.world_root;
+    v.lights_root = hw.lights_root;
+    v.background_tex = bg;
+    v.stack_need = hw.stack_need;
+    d->blob_bytes = blob.size();
+    d->n_prims = hw.n_prims;
+    d->world = world;
+    d->lights = lights;
+    d->background = bg;
+    d->generation = s->generation;
+    flatten_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+// Camera::initilize (camera.rs:204-245)
+static int32_t init_frame(const rt_camera* c, const rt_render_opts* o, rtk_frame_desc& f) {
+    if (!c) return set_error(RT_EINVAL, "null camera");
+    if (c->image_width == 0 || !(c->aspect_ratio > 0)) return set_error(RT_EINVAL, "bad image size");
+    const double PI = 3.14159265358979323846;
+    const uint32_t W = c->image_width, H = rt_camera_image_height(c);
+    std::memset(&f, 0, sizeof f);
+    f.W = W;
+    f.row_stride = (o && o->row_stride > 1) ? o->row_stride : 1;
+    f.row_offset = o ? o->row_offset : 0;
+    f.rows = rt_shard_rows(c, o);
+    f.S = (uint32_t)std::sqrt((double)c->samples_per_pixel);
+    f.max_depth = c->max_depth;
+    f.seed = o ? o->seed : 1;
+    f.pixel_sample_scale = 1.0 / (double)(f.S * f.S);
+    f.recip_sqrt_spp = 1.0 / (double)f.S;
+    if ((uint64_t)W * f.rows * f.S >= 0xFFF00000ull) return set_error(RT_EINVAL, "frame too large for one launch");
+    V3 from(c->look_from), at(c->look_at), up(c->vec_up);
+    double theta = c->vertical_fov_in_degrees * (PI / 180.0);
+    double h = std::tan(theta / 2.0);
+    double vh = 2.0 * h * c->focus_distance;
+    double vw = vh * ((double)W / (double)H);
+    V3 w = div(from - at, length(from - at));
+    if (!finite(w)) return set_error(RT_EPANIC, "Camera axis w should be normalizable!");
+    V3 uc = cross(up, w);
+    V3 u = div(uc, length(uc));
+    if (!finite(u)) return set_error(RT_EPANIC, "Camera axis u should be normalizable!");
+    V3 v = cross(w, u);
+    V3 vu = vw * u, vv = vh * (-v);
+    V3 du = div(vu, (double)W), dv = div(vv, (double)H);
+    V3 ul = ((from - c->focus_distance * w) - div(vu, 2.0)) - div(vv, 2.0);
+    V3 p00 = ul + 0.5 * (du + dv);
+    double radius = c->focus_distance * std::tan((c->defocus_angle_in_degrees / 2.0) * (PI / 180.0));
+    V3 disk_u = radius * u, disk_v = radius * v;
+    auto cp = [](double* dst, V3 x) {
+        dst[0] = x.x;
+        dst[1] = x.y;
+        dst[2] = x.z;
+    };
+    cp(f.center, from);
+    cp(f.pixel00, p00);
+    cp(f.du, du);
+    cp(f.dv, dv);
+    cp(f.disk_u, disk_u);
+    cp(f.disk_v, disk_v);
+    f.defocus = c->defocus_angle_in_degrees > 0.0 ? 1 : 0;
+    return RT_OK;
+}
+
+static int32_t ensure_buffers(DeviceWorld* d, const rtk_frame_desc& f, bool need_out) {
+    hipError_t e;
+    size_t pb = (size_t)f.W * f.rows * f.S * 3 * sizeof(double);
+    if (pb > d->partial_bytes) {
+        if (d->partial) (void)hipFree(d->partial);
+        d->partial = nullptr;
+        d->partial_bytes = 0;
+        if ((e = hipMalloc(&d->partial, pb)) != hipSuccess) return hip_fail(e, "hipMalloc partial sums");
+        d->partial_bytes = pb;
+    }
+    size_t ob = (size_t)f.W * f.rows * 3 * sizeof(float);
+    if (need_out && ob > d->out_bytes) {
+        if (d->out) (void)hipFree(d->out);
+        d->out = nullptr;
+        d->out_bytes = 0;
+        if ((e = hipMalloc(&d->out, ob)) != hipSuccess) return hip_fail(e, "hipMalloc output");
+        d->out_bytes = ob;
+    }
+    return RT_OK;
+}
+
+// sRGB OETF + u8 (utils/color.rs:14-36; palette restated, parity unpinned)
+static uint8_t srgb_u8(double x, int toon) {
+    if (toon == 1) {
+        double m = (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14);
+        x = std::clamp(m, 0.0, 1.0);
+    }
+    double s = x <= 0.0031308 ? 12.92 * x : 1.055 * std::pow(x, 1.0 / 2.4) - 0.055;
+    double q = std::round(s * 255.0);
+    return (uint8_t)std::clamp(q, 0.0, 255.0);
+}
+
+static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
+                      float* dev_out, hipStream_t stream) {
+    if (!s) return set_error(RT_EINVAL, "null scene");
+    if (world < 0 || (size_t)world >= s->objs.size() || s->objs[world].hidden)
+        return set_error(RT_EHANDLE, "unknown world handle");
+    if (s->objs[world].moved) return set_error(RT_EMOVED, "world handle was moved");
+    if (lights != -1) {
+        if (lights < 0 || (size_t)lights >= s->objs.size() || s->objs[lights].hidden)
+            return set_error(RT_EHANDLE, "unknown lights handle");
+        if (s->objs[lights].moved) return set_error(RT_EMOVED, "lights handle was moved");
+    }
+    rtk_frame_desc f;
+    int32_t rc = init_frame(cam, opts, f);
+    if (rc != RT_OK) return rc;
+    if (cam->background_tex != -1 && (cam->background_tex < 0 || (size_t)cam->background_tex >= s->texs.size()))
+        return set_error(RT_EHANDLE, "unknown background texture");
+    double flatten_ms = 0;
+    if ((rc = prepare(s, world, lights, cam->background_tex, flatten_ms)) != RT_OK) return rc;
+    DeviceWorld* d = s->dev;
+    if ((rc = ensure_buffers(d, f, dev_out == nullptr)) != RT_OK) return rc;
+    hipError_t e = hipMemsetAsync(d->stats, 0, 2 * sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync stats");
+    f.ev_start = d->ev_start;
+    f.ev_stop = d->ev_stop;
+    d->pending_t0 = std::chrono::steady_clock::now();
+    d->pending_stream = stream;
+    float* out = dev_out ? dev_out : d->out;
+    const bool run = f.rows > 0 && f.max_depth > 0;
+    if (run) {
+        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->grid);
+        if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    } else if (f.rows > 0) {
+        // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)
+        e = hipMemsetAsync(out, 0, (size_t)f.W * f.rows * 3 * sizeof(float), stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync output");
+    }
+    d->pending = run;
+    d->pending_samples = (uint64_t)f.W * f.rows * f.S * f.S;
+    d->pending_flatten_ms = flatten_ms;
+    return RT_OK;
+}
+
+static int32_t wait(rt_scene* s, rt_stats* st) {
+    DeviceWorld* d = s ? s->dev : nullptr;
+    if (st) std::memset(st, 0, sizeof(*st));
+    if (!d) return set_error(RT_EINVAL, "nothing rendered on this scene");
+    hipError_t e = hipStreamSynchronize(d->pending_stream);
+    if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
+    unsigned long long h[2] = {0, 0};
+    if ((e = hipMemcpy(h, d->stats, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "stats copy");
+    float ms = 0;
+    if (d->pending) (void)hipEventElapsedTime(&ms, d->ev_start, d->ev_stop);
+    if (st) {
+        st->samples = d->pending_samples;
+        st->rays = h[0];
+        st->panics = h[1];
+        st->kernel_ms = ms;
+        st->flatten_ms = d->pending_flatten_ms;
+        st->render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d->pending_t0).count();
+    }
+    d->pending = false;
+    if (h[1]) return set_error(RT_EPANIC, std::to_string(h[1]) + " path(s) hit a reference panic condition "
+                                                                "(NaN radiance, zero pdf, non-normalizable vector)");
+    return RT_OK;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+extern "C" {
+
+int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
+                         float* out_dev) {
+    if (!out_dev) return set_error(RT_EINVAL, "null device output");
+    try {
+        return launch(s, world, lights, cam, opts, out_dev, opts ? (hipStream_t)opts->stream : nullptr);
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
+}
+
+int32_t rt_render_device_wait(rt_scene* s, rt_stats* st) {
+    return wait(s, st);
+}
+
+int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
+                  float* out_lin, uint8_t* out_srgb, rt_stats* st) {
+    try {
+        hipStream_t stream = opts ? (hipStream_t)opts->stream : nullptr;
+        int32_t rc = launch(s, world, lights, cam, opts, nullptr, stream);
+        if (rc != RT_OK) return rc;
+        DeviceWorld* d = s->dev;
+        const uint32_t rows = rt_shard_rows(cam, opts);
+        const size_t n = (size_t)cam->image_width * rows * 3;
+        std::vector<float> host(n);
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return hip_fail(e, "render");
+        if (n && (e = hipMemcpy(host.data(), d->out, n * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy output");
+        int32_t wrc = wait(s, st);
+        if (out_lin) std::memcpy(out_lin, host.data(), n * sizeof(float));
+        if (out_srgb)
+            for (size_t i = 0; i < n; ++i) out_srgb[i] = srgb_u8(host[i], cam->toon_map);
+        return wrc;
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
+}
+
+}  // extern "C"

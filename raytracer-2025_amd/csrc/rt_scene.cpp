@@ -1,0 +1,741 @@
+// rt_scene.cpp -- builder half of the C ABI (include/rt_mi355x.h) and the
+// world flattener.  Host code only; the device half is rt_render.hip.
+#include "rt_scene.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <limits>
+#include <unordered_map>
+
+#include "../../include/rt_mi355x.h"
+
+namespace rth {
+
+static thread_local std::string g_error;
+int32_t set_error(int32_t code, const std::string& msg) {
+    g_error = msg;
+    return code;
+}
+
+static const double INF = std::numeric_limits<double>::infinity();
+
+// aabb.rs:43-51 pad_to_minimums, interval.rs:28-34 expand, 44-46 size
+static Iv pad(Iv t) {
+    const double DELTA = 0.0001;
+    double size = std::fmax(t.hi - t.lo, 0.0);
+    if (size < DELTA) {
+        double p = DELTA / 2.0;
+        return Iv{t.lo - p, t.hi + p};
+    }
+    return t;
+}
+Box3 Box3::empty() {
+    Box3 b;
+    for (auto& i : b.a) i = Iv{INF, -INF};
+    return b;
+}
+Box3 Box3::from_points(V3 p, V3 q) {
+    Box3 b;
+    for (int k = 0; k < 3; ++k) b.a[k] = pad(Iv{std::fmin(p[k], q[k]), std::fmax(p[k], q[k])});
+    return b;
+}
+Box3 Box3::unite(const Box3& o) const {
+    Box3 b;
+    for (int k = 0; k < 3; ++k) b.a[k] = Iv{std::fmin(a[k].lo, o.a[k].lo), std::fmax(a[k].hi, o.a[k].hi)};
+    return b;
+}
+int Box3::longest_axis() const {
+    double lx = std::fmax(a[0].hi - a[0].lo, 0.0), ly = std::fmax(a[1].hi - a[1].lo, 0.0),
+           lz = std::fmax(a[2].hi - a[2].lo, 0.0);
+    if (lx > ly) return lx > lz ? 0 : 2;
+    return ly > lz ? 1 : 2;
+}
+Quat Quat::operator*(const Quat& r) const {
+    return Quat{w * r.w - x * r.x - y * r.y - z * r.z, w * r.x + x * r.w + y * r.z - z * r.y,
+                w * r.y - x * r.z + y * r.w + z * r.x, w * r.z + x * r.y - y * r.x + z * r.w};
+}
+V3 Quat::rotate(V3 v) const {
+    Quat p{0.0, v.x, v.y, v.z};
+    Quat res = (*this * p) * conj();
+    return V3(res.x, res.y, res.z);
+}
+
+// 3x3 matrix of v -> q v q* (for the device; the host keeps the quaternion form)
+static void quat_matrix(const Quat& q, double m[9]) {
+    V3 ex = q.rotate(V3(1, 0, 0)), ey = q.rotate(V3(0, 1, 0)), ez = q.rotate(V3(0, 0, 1));
+    m[0] = ex.x; m[1] = ey.x; m[2] = ez.x;
+    m[3] = ex.y; m[4] = ey.y; m[5] = ez.y;
+    m[6] = ex.z; m[7] = ey.z; m[8] = ez.z;
+}
+
+// total_cmp (f64::total_cmp) used by box_compare, bvh.rs:48-54
+static bool total_less(double a, double b) {
+    int64_t ia, ib;
+    std::memcpy(&ia, &a, 8);
+    std::memcpy(&ib, &b, 8);
+    ia ^= (int64_t)(((uint64_t)(ia >> 63)) >> 1);
+    ib ^= (int64_t)(((uint64_t)(ib >> 63)) >> 1);
+    return ia < ib;
+}
+
+// bvh.rs:16-46 -- returns the object id of the new BVH node
+static int bvh_from_vec(rt_scene* s, std::vector<int> objects) {
+    Box3 bbox = Box3::empty();
+    for (int o : objects) bbox = bbox.unite(s->objs[o].bbox);
+    int axis = bbox.longest_axis();
+    Obj node;
+    node.kind = O_BVH;
+    node.hidden = true;
+    node.bbox = bbox;
+    size_t len = objects.size();
+    if (len == 1) {
+        node.left = objects[0];
+    } else if (len == 2) {
+        node.left = objects[0];
+        node.right = objects[1];
+    } else {
+        std::stable_sort(objects.begin(), objects.end(), [&](int a, int b) {
+            return total_less(s->objs[a].bbox.a[axis].lo, s->objs[b].bbox.a[axis].lo);
+        });
+        size_t mid = len / 2;
+        std::vector<int> lv(objects.begin(), objects.begin() + mid), rv(objects.begin() + mid, objects.end());
+        node.left = bvh_from_vec(s, std::move(lv));
+        node.right = bvh_from_vec(s, std::move(rv));
+    }
+    s->objs.push_back(node);
+    return (int)s->objs.size() - 1;
+}
+
+// ------------------------------------------------------------------ flatten
+namespace {
+struct Flattener {
+    const rt_scene* s;
+    HostWorld& out;
+    std::unordered_map<int, std::pair<uint32_t, uint32_t>> memo;  // obj -> (ref, stack need)
+    std::string err;
+    int32_t code = RT_OK;
+
+    uint32_t fail(int32_t c, const std::string& m) {
+        if (code == RT_OK) {
+            code = c;
+            err = m;
+        }
+        return REF_NONE_;
+    }
+    static constexpr uint32_t REF_NONE_ = rtk::REF_NONE;
+
+    // Returns (ref, need) where need = traversal-stack entries used below the
+    // entry that held this ref (see rt_kernel.hip traverse()).
+    std::pair<uint32_t, uint32_t> emit(int id, bool in_boundary) {
+        auto it = memo.find(id);
+        if (it != memo.end()) return it->second;
+        const Obj& o = s->objs[id];
+        std::pair<uint32_t, uint32_t> r{REF_NONE_, 0};
+        switch (o.kind) {
+            case O_SPHERE: {
+                uint32_t idx = (uint32_t)out.spheres.size();
+                out.spheres.push_back(make_double4(o.c1.x, o.c1.y, o.c1.z, o.radius));
+                out.sphere_mat.push_back(o.mat);
+                r = {rtk::make_ref(rtk::K_SPHERE, idx), 0};
+                ++out.n_prims;
+                break;
+            }
+            case O_MSPHERE: {
+                uint32_t idx = (uint32_t)out.msph_center.size();
+                out.msph_center.push_back(make_double4(o.c1.x, o.c1.y, o.c1.z, o.radius));
+                out.msph_dir.push_back(make_double4(o.cdir.x, o.cdir.y, o.cdir.z, 0.0));
+                out.msph_mat.push_back(o.mat);
+                r = {rtk::make_ref(rtk::K_MSPHERE, idx), 0};
+                ++out.n_prims;
+                break;
+            }
+            case O_QUAD:
+            case O_TRI: {
+                uint32_t idx = (uint32_t)out.planars.size();
+                rtk::DPlanar p;
+                double f[16] = {o.normal.x, o.normal.y, o.normal.z, o.D,  o.anchor.x, o.anchor.y, o.anchor.z, o.u.x,
+                                o.u.y,      o.u.z,      o.v.x,      o.v.y, o.v.z,      o.w.x,      o.w.y,      o.w.z};
+                std::memcpy(p.f, f, sizeof f);
+                out.planars.push_back(p);
+                out.planar_area.push_back(o.area);
+                out.planar_mat.push_back(o.mat);
+                r = {rtk::make_ref(o.kind == O_QUAD ? rtk::K_QUAD : rtk::K_TRI, idx), 0};
+                ++out.n_prims;
+                break;
+            }
+            case O_LIST: {
+                std::vector<std::pair<uint32_t, uint32_t>> kids;
+                for (int c : o.children) kids.push_back(emit(c, in_boundary));
+                uint32_t start = (uint32_t)out.list_children.size();
+                for (auto& k : kids) out.list_children.push_back(k.first);
+                out.list_children.push_back(REF_NONE_);
+                // iterator form: popping (LIST,p) pushes (LIST,p+1) then child p
+                uint32_t need = 0;
+                for (size_t i = 0; i < kids.size(); ++i) {
+                    bool last = i + 1 == kids.size();
+                    uint32_t here = last ? std::max<uint32_t>(1, kids[i].second) : std::max<uint32_t>(2, 1 + kids[i].second);
+                    need = std::max(need, here);
+                }
+                r = {rtk::make_ref(rtk::K_LIST, start), need};
+                break;
+            }
+            case O_BVH: {
+                uint32_t idx = (uint32_t)out.nodes.size();
+                out.nodes.emplace_back();
+                auto L = o.left >= 0 ? emit(o.left, in_boundary) : std::pair<uint32_t, uint32_t>{REF_NONE_, 0};
+                auto R = o.right >= 0 ? emit(o.right, in_boundary) : std::pair<uint32_t, uint32_t>{REF_NONE_, 0};
+                rtk::DNode& n = out.nodes[idx];
+                for (int k = 0; k < 3; ++k) {
+                    n.lo[k] = o.bbox.a[k].lo;
+                    n.hi[k] = o.bbox.a[k].hi;
+                }
+                n.left = L.first;
+                n.right = R.first;
+                uint32_t need = o.right >= 0 ? std::max<uint32_t>(2, std::max(1 + L.second, R.second))
+                                             : std::max<uint32_t>(1, L.second);
+                r = {rtk::make_ref(rtk::K_BVH, idx), need};
+                break;
+            }
+            case O_XFORM: {
+                auto C = emit(o.child, in_boundary);
+                uint32_t idx = (uint32_t)out.xforms.size();
+                rtk::DXform x{};
+                x.off[0] = o.offset.x; x.off[1] = o.offset.y; x.off[2] = o.offset.z;
+                x.scale[0] = o.scale.x; x.scale[1] = o.scale.y; x.scale[2] = o.scale.z;
+                quat_matrix(o.q, x.rot);
+                quat_matrix(o.q.conj(), x.rinv);
+                x.child = C.first;
+                out.xforms.push_back(x);
+                r = {rtk::make_ref(rtk::K_XFORM, idx), std::max<uint32_t>(2, 1 + C.second)};
+                break;
+            }
+            case O_MEDIUM: {
+                if (in_boundary) return {fail(RT_EUNSUPPORTED, "ConstantMedium inside a medium boundary"), 0};
+                auto B = emit(o.child, true);
+                uint32_t idx = (uint32_t)out.media.size();
+                rtk::DMedium m{};
+                m.neg_inv_density = o.neg_inv_density;
+                m.boundary = B.first;
+                m.phase_mat = o.phase_mat;
+                m.medium_id = o.medium_id;
+                out.media.push_back(m);
+                r = {rtk::make_ref(rtk::K_MEDIUM, idx), std::max<uint32_t>(1, B.second)};
+                break;
+            }
+        }
+        memo[id] = r;
+        return r;
+    }
+};
+
+bool light_ok(const rt_scene* s, int id, int depth) {
+    const Obj& o = s->objs[id];
+    switch (o.kind) {
+        case O_SPHERE:
+        case O_QUAD:
+        case O_TRI: return true;
+        case O_LIST:
+            if (depth > 0 || o.children.empty()) return false;
+            for (int c : o.children)
+                if (!light_ok(s, c, depth + 1)) return false;
+            return true;
+        default: return false;
+    }
+}
+}  // namespace
+
+static int tex_needs_uv(const rt_scene* s, int t, int depth = 0) {
+    if (t < 0 || depth > 16) return 0;
+    const TexRec& r = s->texs[t];
+    if (r.type == rtk::T_IMAGE) return r.h != 0;
+    if (r.type == rtk::T_CHECKER) return tex_needs_uv(s, r.even, depth + 1) | tex_needs_uv(s, r.odd, depth + 1);
+    return 0;
+}
+
+int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, HostWorld& out) {
+    out = HostWorld();
+    // textures (texture.rs) and materials (material.rs) keep their handle ids
+    for (size_t i = 0; i < s->texs.size(); ++i) {
+        const TexRec& r = s->texs[i];
+        rtk::DTexture t{};
+        t.type = r.type;
+        for (int k = 0; k < 3; ++k) {
+            t.color[k] = r.color[k];
+            t.color2[k] = r.color2[k];
+        }
+        t.scale = r.scale;
+        t.a = r.type == rtk::T_CHECKER ? r.even : (int32_t)r.w;
+        t.b = r.type == rtk::T_CHECKER ? r.odd : (int32_t)r.h;
+        t.c = r.linear;
+        t.data = r.type == rtk::T_IMAGE ? r.texel_offset : (uint64_t)(r.perlin < 0 ? 0 : r.perlin);
+        t.needs_uv = tex_needs_uv(s, (int)i);
+        out.textures.push_back(t);
+    }
+    out.texels = s->texels;
+    out.perlin = s->perlins;
+    for (size_t i = 0; i < s->mats.size(); ++i) {
+        const MatRec& r = s->mats[i];
+        rtk::DMaterial m{};
+        m.type = r.type;
+        m.tex = r.tex;
+        m.inner = r.inner;
+        m.inner2 = r.inner2;
+        for (int k = 0; k < 3; ++k) m.albedo[k] = r.albedo[k];
+        m.fuzz = r.param;
+        out.materials.push_back(m);
+    }
+    // flags: uv need and emission, resolved through DiffuseLight/Mix nesting
+    for (size_t i = 0; i < out.materials.size(); ++i) {
+        rtk::DMaterial& m = out.materials[i];
+        uint32_t f = 0;
+        if (m.tex >= 0 && tex_needs_uv(s, m.tex)) f |= rtk::MF_NEEDS_UV;
+        if (m.type == rtk::M_DIFFUSE_LIGHT) f |= rtk::MF_EMISSIVE;
+        m.flags = f;
+    }
+    for (int pass = 0; pass < 4; ++pass)
+        for (size_t i = 0; i < out.materials.size(); ++i) {
+            rtk::DMaterial& m = out.materials[i];
+            if (m.type == rtk::M_DIFFUSE_LIGHT || m.type == rtk::M_MIX) {
+                for (int sub : {m.inner, m.inner2})
+                    if (sub >= 0) m.flags |= out.materials[sub].flags & (rtk::MF_NEEDS_UV | rtk::MF_EMISSIVE);
+            }
+        }
+    for (size_t i = 0; i < out.materials.size(); ++i) {
+        const rtk::DMaterial& m = out.materials[i];
+        if (m.type == rtk::M_MIX) {
+            for (int sub : {m.inner, m.inner2}) {
+                int st = out.materials[sub].type;
+                if (st == rtk::M_MIX || (st == rtk::M_DIFFUSE_LIGHT && out.materials[sub].inner >= 0))
+                    return set_error(RT_EUNSUPPORTED, "Mix of Mix / of DiffuseLight-with-material is not on the kernel path yet");
+            }
+        }
+        if (m.type == rtk::M_DIFFUSE_LIGHT && m.inner >= 0) {
+            int st = out.materials[m.inner].type;
+            if (st == rtk::M_MIX || st == rtk::M_DIFFUSE_LIGHT)
+                return set_error(RT_EUNSUPPORTED, "DiffuseLight wrapping Mix/DiffuseLight is not on the kernel path yet");
+        }
+    }
+    if (background_tex >= (int32_t)s->texs.size()) return set_error(RT_EHANDLE, "unknown background texture");
+
+    Flattener F{s, out, {}, {}, RT_OK};
+    auto W = F.emit(world, false);
+    if (F.code != RT_OK) return set_error(F.code, F.err);
+    out.world_root = W.first;
+    out.stack_need = 1 + W.second;
+    out.lights_root = rtk::REF_NONE;
+    if (lights >= 0) {
+        if (!light_ok(s, lights, 0))
+            return set_error(RT_EUNSUPPORTED,
+                             "lights must be a Sphere/Quad/Triangle or a non-empty Hittables of them on the kernel path");
+        auto Lr = F.emit(lights, false);
+        if (F.code != RT_OK) return set_error(F.code, F.err);
+        out.lights_root = Lr.first;
+    }
+    if (out.list_children.empty()) out.list_children.push_back(rtk::REF_NONE);
+    return RT_OK;
+}
+
+}  // namespace rth
+
+using namespace rth;
+
+// ------------------------------------------------------------------ C ABI (builders)
+namespace {
+bool bad(const double* p) { return p == nullptr; }
+int32_t check_obj(const rt_scene* s, int32_t o) {
+    if (o < 0 || (size_t)o >= s->objs.size() || s->objs[o].hidden) return set_error(RT_EHANDLE, "unknown object handle");
+    if (s->objs[o].moved) return set_error(RT_EMOVED, "object handle already moved (Box<dyn Hittable> is owned)");
+    return RT_OK;
+}
+bool tex_ok(const rt_scene* s, int32_t t) { return t >= 0 && (size_t)t < s->texs.size(); }
+bool mat_ok(const rt_scene* s, int32_t m) { return m >= 0 && (size_t)m < s->mats.size(); }
+int32_t push_obj(rt_scene* s, Obj o) {
+    s->objs.push_back(std::move(o));
+    ++s->generation;
+    return (int32_t)s->objs.size() - 1;
+}
+int32_t push_tex(rt_scene* s, TexRec t) {
+    s->texs.push_back(t);
+    ++s->generation;
+    return (int32_t)s->texs.size() - 1;
+}
+int32_t push_mat(rt_scene* s, MatRec m) {
+    s->mats.push_back(m);
+    ++s->generation;
+    return (int32_t)s->mats.size() - 1;
+}
+Obj make_planar(ObjKind k, V3 q, V3 u, V3 v, int mat) {
+    Obj o;
+    o.kind = k;
+    V3 n = cross(u, v);
+    o.normal = div(n, length(n));
+    o.D = dot(o.normal, q);
+    o.w = div(n, dot(n, n));
+    o.area = k == O_QUAD ? length(n) : length(n) / 2.0;
+    o.anchor = q;
+    o.u = u;
+    o.v = v;
+    o.mat = mat;
+    if (k == O_QUAD)  // quad.rs:50-55
+        o.bbox = Box3::from_points(q, q + u + v).unite(Box3::from_points(q + u, q + v));
+    else  // triangle.rs:49-54
+        o.bbox = Box3::from_points(q, q + u).unite(Box3::from_points(q, q + v));
+    return o;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return rth::g_error.c_str(); }
+rt_scene* rt_scene_create(void) {
+    try {
+        return new rt_scene();
+    } catch (...) {
+        set_error(RT_ENOMEM, "out of memory");
+        return nullptr;
+    }
+}
+
+// ---- textures
+int32_t rt_tex_solid(rt_scene* s, const double rgb[3]) {
+    if (!s || bad(rgb)) return set_error(RT_EINVAL, "null argument");
+    TexRec t{};
+    t.type = rtk::T_SOLID;
+    std::memcpy(t.color, rgb, 24);
+    return push_tex(s, t);
+}
+int32_t rt_tex_checker(rt_scene* s, double scale, int32_t even, int32_t odd) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!tex_ok(s, even) || !tex_ok(s, odd)) return set_error(RT_EHANDLE, "unknown texture");
+    TexRec t{};
+    t.type = rtk::T_CHECKER;
+    t.scale = 1.0 / scale;  // inv_scale (texture.rs:52)
+    t.even = even;
+    t.odd = odd;
+    return push_tex(s, t);
+}
+int32_t rt_tex_image(rt_scene* s, uint32_t w, uint32_t h, const float* rgba, int32_t linear) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if ((w == 0) != (h == 0)) return set_error(RT_EINVAL, "image must have both dimensions or none");
+    if (w && !rgba) return set_error(RT_EINVAL, "null pixels");
+    TexRec t{};
+    t.type = rtk::T_IMAGE;
+    t.w = w;
+    t.h = h;
+    t.linear = linear != 0;
+    t.texel_offset = s->texels.size();
+    if (w) s->texels.insert(s->texels.end(), rgba, rgba + (size_t)w * h * 4);
+    return push_tex(s, t);
+}
+int32_t rt_tex_noise(rt_scene* s, double scale, uint64_t seed) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    // perlin.rs:16-36 drawn from SplitMix64(seed) (the RNG contract)
+    rtk::DPerlin p{};
+    uint64_t st = seed;
+    auto next = [&st]() {
+        uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z = z ^ (z >> 31);
+        return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    };
+    const double PI = 3.14159265358979323846;
+    for (int i = 0; i < 256; ++i) {
+        double r1 = next(), r2 = next();
+        p.randvec[i][0] = std::cos(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
+        p.randvec[i][1] = std::sin(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
+        p.randvec[i][2] = 1.0 - 2.0 * r2;
+    }
+    for (int a = 0; a < 3; ++a) {
+        for (int i = 0; i < 256; ++i) p.perm[a][i] = i;
+        for (int i = 255; i >= 1; --i) {
+            int target = (int)(next() * (double)(i + 1));
+            if (target > i) target = i;
+            std::swap(p.perm[a][i], p.perm[a][target]);
+        }
+    }
+    s->perlins.push_back(p);
+    TexRec t{};
+    t.type = rtk::T_NOISE;
+    t.scale = scale;
+    t.perlin = (int)s->perlins.size() - 1;
+    return push_tex(s, t);
+}
+int32_t rt_tex_sky_gradient(rt_scene* s, const double horizon[3], const double zenith[3]) {
+    if (!s || bad(horizon) || bad(zenith)) return set_error(RT_EINVAL, "null argument");
+    TexRec t{};
+    t.type = rtk::T_SKY;
+    std::memcpy(t.color, horizon, 24);
+    std::memcpy(t.color2, zenith, 24);
+    return push_tex(s, t);
+}
+
+// ---- materials
+int32_t rt_mat_empty(rt_scene* s) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    MatRec m{};
+    m.type = rtk::M_EMPTY;
+    return push_mat(s, m);
+}
+int32_t rt_mat_lambertian(rt_scene* s, int32_t tex) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!tex_ok(s, tex)) return set_error(RT_EHANDLE, "unknown texture");
+    MatRec m{};
+    m.type = rtk::M_LAMBERTIAN;
+    m.tex = tex;
+    return push_mat(s, m);
+}
+int32_t rt_mat_metal(rt_scene* s, const double albedo[3], double fuzz) {
+    if (!s || bad(albedo)) return set_error(RT_EINVAL, "null argument");
+    MatRec m{};
+    m.type = rtk::M_METAL;
+    std::memcpy(m.albedo, albedo, 24);
+    m.param = std::clamp(fuzz, 0.0, 1.0);  // material.rs:77
+    return push_mat(s, m);
+}
+int32_t rt_mat_dielectric(rt_scene* s, int32_t tex, double ior) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!tex_ok(s, tex)) return set_error(RT_EHANDLE, "unknown texture");
+    MatRec m{};
+    m.type = rtk::M_DIELECTRIC;
+    m.tex = tex;
+    m.param = ior;
+    return push_mat(s, m);
+}
+int32_t rt_mat_diffuse_light(rt_scene* s, int32_t tex, int32_t inner) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!tex_ok(s, tex)) return set_error(RT_EHANDLE, "unknown texture");
+    if (inner != -1 && !mat_ok(s, inner)) return set_error(RT_EHANDLE, "unknown material");
+    MatRec m{};
+    m.type = rtk::M_DIFFUSE_LIGHT;
+    m.tex = tex;
+    m.inner = inner;
+    return push_mat(s, m);
+}
+int32_t rt_mat_isotropic(rt_scene* s, int32_t tex) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!tex_ok(s, tex)) return set_error(RT_EHANDLE, "unknown texture");
+    MatRec m{};
+    m.type = rtk::M_ISOTROPIC;
+    m.tex = tex;
+    return push_mat(s, m);
+}
+int32_t rt_mat_transparent(rt_scene* s) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    MatRec m{};
+    m.type = rtk::M_TRANSPARENT;
+    return push_mat(s, m);
+}
+int32_t rt_mat_mix(rt_scene* s, int32_t m1, int32_t m2, double ratio) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, m1) || !mat_ok(s, m2)) return set_error(RT_EHANDLE, "unknown material");
+    MatRec m{};
+    m.type = rtk::M_MIX;
+    m.inner = m1;
+    m.inner2 = m2;
+    m.param = ratio;
+    return push_mat(s, m);
+}
+
+// ---- hittables
+int32_t rt_sphere(rt_scene* s, const double c[3], double r, int32_t mat) {
+    if (!s || bad(c)) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, mat)) return set_error(RT_EHANDLE, "unknown material");
+    Obj o;
+    o.kind = O_SPHERE;
+    o.c1 = V3(c);
+    o.radius = std::fmax(0.0, r);
+    o.mat = mat;
+    V3 rv(r, r, r);
+    o.bbox = Box3::from_points(o.c1 - rv, o.c1 + rv);  // sphere.rs:31
+    return push_obj(s, o);
+}
+int32_t rt_sphere_moving(rt_scene* s, const double c1[3], const double c2[3], double r, int32_t mat) {
+    if (!s || bad(c1) || bad(c2)) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, mat)) return set_error(RT_EHANDLE, "unknown material");
+    Obj o;
+    o.kind = O_MSPHERE;
+    o.c1 = V3(c1);
+    o.cdir = V3(c2) - V3(c1);
+    o.radius = std::fmax(0.0, r);
+    o.mat = mat;
+    V3 rv(r, r, r);
+    V3 at0 = o.c1 + 0.0 * o.cdir, at1 = o.c1 + 1.0 * o.cdir;  // sphere.rs:44-47
+    o.bbox = Box3::from_points(at0 - rv, at0 + rv).unite(Box3::from_points(at1 - rv, at1 + rv));
+    return push_obj(s, o);
+}
+int32_t rt_quad(rt_scene* s, const double q[3], const double u[3], const double v[3], int32_t mat) {
+    if (!s || bad(q) || bad(u) || bad(v)) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, mat)) return set_error(RT_EHANDLE, "unknown material");
+    V3 n = cross(V3(u), V3(v));
+    if (!finite(div(n, length(n)))) return set_error(RT_EPANIC, "The length of normal should be normalizable!");
+    return push_obj(s, make_planar(O_QUAD, V3(q), V3(u), V3(v), mat));
+}
+int32_t rt_triangle(rt_scene* s, const double a[3], const double u[3], const double v[3], int32_t mat) {
+    if (!s || bad(a) || bad(u) || bad(v)) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, mat)) return set_error(RT_EHANDLE, "unknown material");
+    V3 n = cross(V3(u), V3(v));
+    if (!finite(div(n, length(n)))) return set_error(RT_EDEGENERATE, "degenerate triangle (Triangle::new -> None)");
+    return push_obj(s, make_planar(O_TRI, V3(a), V3(u), V3(v), mat));
+}
+int32_t rt_hittables_new(rt_scene* s) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    Obj o;
+    o.kind = O_LIST;  // bbox = AABB::default() (hits.rs:9)
+    return push_obj(s, o);
+}
+int32_t rt_hittables_add(rt_scene* s, int32_t list, int32_t object) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    int32_t rc;
+    if ((rc = check_obj(s, list)) != RT_OK) return rc;
+    if ((rc = check_obj(s, object)) != RT_OK) return rc;
+    if (s->objs[list].kind != O_LIST) return set_error(RT_EHANDLE, "not a Hittables object");
+    if (list == object) return set_error(RT_EINVAL, "cannot add a list to itself");
+    s->objs[list].bbox = s->objs[list].bbox.unite(s->objs[object].bbox);  // hits.rs:28
+    s->objs[list].children.push_back(object);
+    s->objs[object].moved = true;
+    ++s->generation;
+    return RT_OK;
+}
+int32_t rt_bvh_new(rt_scene* s, int32_t list) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    int32_t rc;
+    if ((rc = check_obj(s, list)) != RT_OK) return rc;
+    if (s->objs[list].kind != O_LIST) return set_error(RT_EHANDLE, "not a Hittables object");
+    if (s->objs[list].children.empty()) return set_error(RT_EPANIC, "BVH node must contain at least one object");
+    std::vector<int> objs = s->objs[list].children;
+    s->objs[list].moved = true;
+    int root = bvh_from_vec(s, std::move(objs));
+    s->objs[root].hidden = false;
+    ++s->generation;
+    return root;
+}
+int32_t rt_build_box(rt_scene* s, const double a[3], const double b[3], int32_t mat) {
+    if (!s || bad(a) || bad(b)) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, mat)) return set_error(RT_EHANDLE, "unknown material");
+    // quad.rs:128-189
+    V3 mn(std::fmin(a[0], b[0]), std::fmin(a[1], b[1]), std::fmin(a[2], b[2]));
+    V3 mx(std::fmax(a[0], b[0]), std::fmax(a[1], b[1]), std::fmax(a[2], b[2]));
+    V3 dx(mx.x - mn.x, 0, 0), dy(0, mx.y - mn.y, 0), dz(0, 0, mx.z - mn.z);
+    int32_t list = rt_hittables_new(s);
+    const V3 anchors[6] = {V3(mn.x, mn.y, mx.z), V3(mx.x, mn.y, mx.z), V3(mx.x, mn.y, mn.z),
+                           V3(mn.x, mn.y, mn.z), V3(mn.x, mx.y, mx.z), V3(mn.x, mn.y, mn.z)};
+    const V3 us[6] = {dx, -dz, -dx, dz, dx, dx};
+    const V3 vs[6] = {dy, dy, dy, dy, -dz, dz};
+    for (int k = 0; k < 6; ++k) {
+        double q[3] = {anchors[k].x, anchors[k].y, anchors[k].z}, u[3] = {us[k].x, us[k].y, us[k].z},
+               v[3] = {vs[k].x, vs[k].y, vs[k].z};
+        int32_t side = rt_quad(s, q, u, v, mat);
+        if (side < 0) return side;
+        rt_hittables_add(s, list, side);
+    }
+    return list;
+}
+int32_t rt_transform_new(rt_scene* s, int32_t object, const double* off, const double* q, const double* sc) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    int32_t rc;
+    if ((rc = check_obj(s, object)) != RT_OK) return rc;
+    Obj o;
+    o.kind = O_XFORM;
+    o.child = object;
+    o.offset = off ? V3(off) : V3(0, 0, 0);
+    o.q = q ? Quat{q[0], q[1], q[2], q[3]} : Quat{};
+    o.scale = sc ? V3(sc) : V3(1, 1, 1);
+    // shapes.rs:49-72: AABB of the 8 transformed corners
+    const Box3& cb = s->objs[object].bbox;
+    V3 mn(INF, INF, INF), mx(-INF, -INF, -INF);
+    for (int i = 0; i < 8; ++i) {
+        V3 p(cb.a[0].lo, cb.a[1].lo, cb.a[2].lo);
+        if (i & 4) p.x = cb.a[0].hi;
+        if (i & 2) p.y = cb.a[1].hi;
+        if (i & 1) p.z = cb.a[2].hi;
+        V3 t = o.q.rotate(p * o.scale) + o.offset;
+        mn = V3(std::fmin(mn.x, t.x), std::fmin(mn.y, t.y), std::fmin(mn.z, t.z));
+        mx = V3(std::fmax(mx.x, t.x), std::fmax(mx.y, t.y), std::fmax(mx.z, t.z));
+    }
+    o.bbox = Box3::from_points(mn, mx);
+    s->objs[object].moved = true;
+    return push_obj(s, o);
+}
+int32_t rt_constant_medium_new(rt_scene* s, int32_t boundary, double density, int32_t tex) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    int32_t rc;
+    if ((rc = check_obj(s, boundary)) != RT_OK) return rc;
+    if (!tex_ok(s, tex)) return set_error(RT_EHANDLE, "unknown texture");
+    Obj o;
+    o.kind = O_MEDIUM;
+    o.child = boundary;
+    o.bbox = s->objs[boundary].bbox;  // volume.rs:75-77
+    o.neg_inv_density = -1.0 / density;
+    o.phase_mat = rt_mat_isotropic(s, tex);  // Box<Isotropic> (volume.rs:31)
+    o.medium_id = s->next_medium_id++;
+    s->objs[boundary].moved = true;
+    return push_obj(s, o);
+}
+
+int32_t rt_quat_from_axis_angle(const double axis[3], double deg, double out[4]) {
+    if (bad(axis) || !out) return set_error(RT_EINVAL, "null argument");
+    // quaternion.rs:40-53
+    const double PI = 3.14159265358979323846;
+    double half = deg * (PI / 180.0) * 0.5;
+    double sn = std::sin(half), c = std::cos(half);
+    V3 a(axis);
+    V3 u = div(a, length(a));
+    if (!finite(u)) return set_error(RT_EPANIC, "Quaternion::from_axis_angle: axis not normalizable");
+    out[0] = c;
+    out[1] = u.x * sn;
+    out[2] = u.y * sn;
+    out[3] = u.z * sn;
+    return RT_OK;
+}
+void rt_quat_from_euler(double yaw, double pitch, double roll, double out[4]) {
+    // quaternion.rs:23-38
+    double cy = std::cos(0.5 * yaw), sy = std::sin(0.5 * yaw);
+    double cp = std::cos(0.5 * pitch), sp = std::sin(0.5 * pitch);
+    double cr = std::cos(0.5 * roll), sr = std::sin(0.5 * roll);
+    out[0] = cr * cp * cy + sr * sp * sy;
+    out[1] = sr * cp * cy - cr * sp * sy;
+    out[2] = cr * sp * cy + sr * cp * sy;
+    out[3] = cr * cp * sy - sr * sp * cy;
+}
+
+void rt_camera_default(rt_camera* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->aspect_ratio = 1.0;  // camera.rs:76-104
+    c->image_width = 100;
+    c->samples_per_pixel = 10;
+    c->max_depth = 10;
+    c->background_tex = -1;
+    c->vertical_fov_in_degrees = 90.0;
+    c->look_at[2] = -1.0;
+    c->vec_up[1] = 1.0;
+    c->focus_distance = 10.0;
+}
+uint32_t rt_camera_image_height(const rt_camera* c) {
+    if (!c || !(c->aspect_ratio > 0)) return 1;
+    uint32_t h = (uint32_t)((double)c->image_width / c->aspect_ratio);  // camera.rs:205-210
+    return h < 1 ? 1 : h;
+}
+void rt_render_opts_default(rt_render_opts* o) {
+    if (!o) return;
+    std::memset(o, 0, sizeof(*o));
+    o->seed = 1;
+    o->row_stride = 1;
+}
+uint32_t rt_shard_rows(const rt_camera* c, const rt_render_opts* o) {
+    uint32_t H = rt_camera_image_height(c);
+    uint32_t stride = (o && o->row_stride > 1) ? o->row_stride : 1;
+    uint32_t off = o ? o->row_offset : 0;
+    if (off >= H) return 0;
+    return (H - off + stride - 1) / stride;
+}
+
+void rt_scene_destroy(rt_scene* s) {
+    if (!s) return;
+    if (s->dev) destroy_device_world(s->dev);
+    delete s;
+}
+
+}  // extern "C"

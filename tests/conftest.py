@@ -1,0 +1,73 @@
+import ctypes
+import importlib
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = "raytracer-2025_amd"
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+def pkg_module(name=""):
+    return importlib.import_module(PKG + ("." + name if name else ""))
+
+
+def _make(path):
+    subprocess.run(["make", "-j", "4", "-C", path], check=True, stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture(scope="session")
+def capi():
+    return pkg_module("capi")
+
+
+@pytest.fixture(scope="session")
+def rt():
+    return pkg_module("raytracer")
+
+
+@pytest.fixture(scope="session")
+def scenes():
+    return pkg_module("scenes")
+
+
+@pytest.fixture(scope="session")
+def oracle(capi):
+    """The TEST-ONLY CPU oracle (oracle/), as the checker."""
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    _make(os.path.join(ROOT, "oracle"))
+    return capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
+
+
+@pytest.fixture(scope="session")
+def product():
+    """librt_mi355x.so through the package loader (fails loudly when missing)."""
+    pkg = pkg_module()
+    if not os.path.exists(pkg.LIB_PATH):
+        _make(os.path.join(ROOT, PKG))
+    return pkg.load()
+
+
+@pytest.fixture(scope="session")
+def gpu(product):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    return product
+
+
+def rmse_per_channel(a, b):
+    import numpy as np
+
+    d = a.astype(np.float64) - b.astype(np.float64)
+    return np.sqrt((d ** 2).reshape(-1, 3).mean(axis=0))
