@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reference-bvh", action="store_true",
+                    help="A/B only: keep the reference BVH topology instead of the SAH rebuild")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-row-stride", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=16)
@@ -134,6 +136,7 @@ def main():
     opts.seed = args.seed
     opts.row_offset = rank
     opts.row_stride = world_size
+    opts.flags = 1 if args.reference_bvh else 0  # RT_FLAG_REFERENCE_BVH
     rows = api.shard_rows(ctypes.byref(c), ctypes.byref(opts))
     out = torch.empty((max(rows, 1), W, 3), dtype=torch.float32, device=device)
     stream = torch.cuda.current_stream(device)
@@ -204,6 +207,7 @@ def main():
                             "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
                 "frame_samples": frame_samples,
                 "parallelism": f"row-shard x{world_size}",
+                "bvh": "reference topology" if args.reference_bvh else "binned SAH, two-box f32 nodes",
             },
             "roofline": {
                 "bound": "valu-fp64",

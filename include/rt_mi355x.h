@@ -98,7 +98,8 @@ int32_t rt_triangle(rt_scene* s, const double anchor[3], const double u[3], cons
 int32_t rt_hittables_new(rt_scene* s);
 /* Hittables::add (hits.rs:27-30); moves `object` */
 int32_t rt_hittables_add(rt_scene* s, int32_t list, int32_t object);
-/* BVH::new(Hittables) (bvh.rs:12-46); moves `list`; same topology as the reference */
+/* BVH::new(Hittables) (bvh.rs:12-46); moves `list`.  The reference topology is
+ * built; rendering rebuilds it with a binned SAH unless RT_FLAG_REFERENCE_BVH. */
 int32_t rt_bvh_new(rt_scene* s, int32_t list);
 /* build_box (shapes/quad.rs:128-189); returns a Hittables object */
 int32_t rt_build_box(rt_scene* s, const double a[3], const double b[3], int32_t mat);
@@ -139,9 +140,14 @@ typedef struct rt_render_opts {
     uint32_t row_offset; /* shard: render rows y = row_offset + k*row_stride */
     uint32_t row_stride; /* 0 or 1 = every row */
     uint32_t threads;    /* CPU implementations only; 0 = all cores */
-    uint32_t flags;      /* reserved, 0 */
+    uint32_t flags;      /* RT_FLAG_* */
     void* stream;        /* hipStream_t for rt_render_device; NULL = default */
 } rt_render_opts;
+
+/* Keep the reference BVH topology (bvh.rs:16-46: longest axis, sort by box
+ * min, median split) instead of the default binned-SAH rebuild of every BVH.
+ * Closest-hit results agree up to exact ties in t; used for A/B measurement. */
+#define RT_FLAG_REFERENCE_BVH 1u
 
 void rt_render_opts_default(rt_render_opts* opts);
 
@@ -164,6 +170,19 @@ typedef struct rt_stats {
  * Objects passed here are borrowed, not moved. */
 int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
                   float* out_linear_rgb, uint8_t* out_srgb, rt_stats* stats);
+
+/* What rt_render would upload for (world, lights): host-only, no device needed. */
+typedef struct rt_world_info {
+    uint64_t device_bytes;    /* size of the flattened world blob */
+    uint32_t bvh_nodes;       /* two-box BVH nodes */
+    uint32_t primitives;      /* spheres + moving spheres + quads + triangles */
+    uint32_t bvh_leaves;      /* objects under BVHs */
+    uint32_t stack_need;      /* traversal-stack entries one lane needs */
+    uint32_t kernel_tier;     /* 0 = spheres/BVH/basic materials, 1 = full */
+    uint32_t features;        /* F_* bits (rt_layout.h) */
+} rt_world_info;
+int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, uint32_t flags,
+                          rt_world_info* out);
 
 /* Number of rows a shard renders (rows of the compact output). */
 uint32_t rt_shard_rows(const rt_camera* cam, const rt_render_opts* opts);

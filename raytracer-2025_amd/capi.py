@@ -31,6 +31,18 @@ class RtCamera(C.Structure):
     ]
 
 
+class RtWorldInfo(C.Structure):
+    _fields_ = [
+        ("device_bytes", C.c_uint64),
+        ("bvh_nodes", C.c_uint32),
+        ("primitives", C.c_uint32),
+        ("bvh_leaves", C.c_uint32),
+        ("stack_need", C.c_uint32),
+        ("kernel_tier", C.c_uint32),
+        ("features", C.c_uint32),
+    ]
+
+
 class RtRenderOpts(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -100,6 +112,7 @@ SIGNATURES = {
     "shard_rows": (_U, [C.POINTER(RtCamera), C.POINTER(RtRenderOpts)]),
     "render_device": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _P]),
     "render_device_wait": (_I, [_P, C.POINTER(RtStats)]),
+    "world_info_get": (_I, [_P, _I, _I, _I, _U, C.POINTER(RtWorldInfo)]),
 }
 
 # Entry points only a CPU implementation has (the oracle).

@@ -6,8 +6,10 @@
 
 #include "rt_layout.h"
 
-#define RT_BLOCK 256  // 4 waves of 64
-#define RT_STACK 32   // traversal-stack entries per lane (LDS: RT_STACK * RT_BLOCK * 4 B = 32 KiB per block)
+#define RT_BLOCK 256        // 4 waves of 64
+// traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
+#define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
+#define RT_STACK_FULL 32    // 64 KiB: 2 blocks per CU
 
 // Camera::initilize results (camera.rs:204-245) for one shard.
 struct rtk_frame_desc {
@@ -21,7 +23,12 @@ struct rtk_frame_desc {
     void* ev_stop;
 };
 
+// tier 0: spheres / lists / BVH, Lambertian / Metal / Dielectric / Empty,
+// solid / sky / checker textures, no lights (C1, C2).  tier 1: everything.
+extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int grid);
-extern "C" int rtk_path_kernel_occupancy(int* blocks_per_cu);
+                                       int tier, int grid, void* params_dev);
+// device bytes rtk_launch_frame needs at params_dev
+extern "C" size_t rtk_params_bytes(void);
+extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);

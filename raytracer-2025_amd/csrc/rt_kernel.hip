@@ -72,6 +72,7 @@ __device__ void image_pixel(const SceneView& S, const DTexture& t, int64_t x, in
     out[3] = px[3];
 }
 
+template <bool FULL>
 __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
     for (int guard = 0; guard < 16; ++guard) {
         const DTexture& t = S.textures[tid];
@@ -87,6 +88,10 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
                 tid = ((xi + yi + zi) % 2 == 0) ? t.a : t.b;
                 continue;
             }
+            default: break;
+        }
+        if constexpr (FULL) {
+          switch (t.type) {
             case T_IMAGE: {
                 if (t.b == 0) return d3(0.0, 1.0, 1.0);  // texture.rs:167-169
                 const double uu = u - floor(u);
@@ -125,28 +130,32 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
                 const double turb = fabs(accum);
                 return (1.0 + sin(t.scale * p.z + 10.0 * turb)) * d3(0.5, 0.5, 0.5);
             }
-            default: return d3(0.0, 0.0, 0.0);
+            default: break;
+          }
         }
+        return d3(0.0, 0.0, 0.0);
     }
     return d3(0.0, 0.0, 0.0);
 }
 
 // ------------------------------------------------------------------ geometry tests
-// aabb.rs:62-78 slab test; inv = 1/d per axis computed once per ray (same value).
-__device__ __forceinline__ bool slab(const DNode& n, const Ray& r, D3 inv, double tmin, double tmax) {
-    double t0 = (n.lo[0] - r.o.x) * inv.x, t1 = (n.hi[0] - r.o.x) * inv.x;
-    double lo = fmax(tmin, fmin(t0, t1)), hi = fmin(tmax, fmax(t0, t1));
-    if (!(lo <= hi)) return false;
-    t0 = (n.lo[1] - r.o.y) * inv.y;
-    t1 = (n.hi[1] - r.o.y) * inv.y;
-    lo = fmax(lo, fmin(t0, t1));
-    hi = fmin(hi, fmax(t0, t1));
-    if (!(lo <= hi)) return false;
-    t0 = (n.lo[2] - r.o.z) * inv.z;
-    t1 = (n.hi[2] - r.o.z) * inv.z;
-    lo = fmax(lo, fmin(t0, t1));
-    hi = fmin(hi, fmax(t0, t1));
-    return lo <= hi;
+// aabb.rs:62-78 slab test on a child box stored f32 (outward-rounded), f64
+// arithmetic; inv = 1/d per axis, computed once per ray (the same value the
+// reference computes per node).  Returns the entry distance in `entry`.
+__device__ __forceinline__ bool slab2(const float* lo, const float* hi, const Ray& r, D3 inv, double tmin,
+                                      double tmax, double& entry) {
+    double t0 = ((double)lo[0] - r.o.x) * inv.x, t1 = ((double)hi[0] - r.o.x) * inv.x;
+    double a = fmax(tmin, fmin(t0, t1)), b = fmin(tmax, fmax(t0, t1));
+    t0 = ((double)lo[1] - r.o.y) * inv.y;
+    t1 = ((double)hi[1] - r.o.y) * inv.y;
+    a = fmax(a, fmin(t0, t1));
+    b = fmin(b, fmax(t0, t1));
+    t0 = ((double)lo[2] - r.o.z) * inv.z;
+    t1 = ((double)hi[2] - r.o.z) * inv.z;
+    a = fmax(a, fmin(t0, t1));
+    b = fmin(b, fmax(t0, t1));
+    entry = a;
+    return a <= b;
 }
 
 // sphere.rs:77-96 -- t of the accepted root, or false
@@ -213,9 +222,60 @@ struct HitInfo {
     uint32_t xf[MAX_XF];
 };
 
-// Closest t of a medium boundary (no media inside, no records).
-__device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax,
-                           uint32_t* stk, uint32_t sp0, double& tbest) {
+// The per-lane traversal stack: entry k of lane l at stk[k * RT_BLOCK] (the
+// pointer is already offset by the lane), {ref, entry distance as f32 rounded
+// down} -- one ds_write_b64 / ds_read_b64 per push / pop, 64 distinct banks
+// per half-wave.
+struct Stack {
+    uint2* base;
+    __device__ __forceinline__ void push(uint32_t sp, uint32_t ref, float t) { base[sp * RT_BLOCK] = make_uint2(ref, __float_as_uint(t)); }
+    __device__ __forceinline__ uint2 at(uint32_t sp) const { return base[sp * RT_BLOCK]; }
+};
+__device__ __forceinline__ float f32_down(double x) {
+    float f = (float)x;  // round-to-nearest; step one ulp down when it rounded up
+    if ((double)f > x) {
+        const uint32_t b = __float_as_uint(f);
+        f = (f > 0.0f) ? __uint_as_float(b - 1u) : (f == 0.0f ? -1.401298464e-45f : __uint_as_float(b + 1u));
+    }
+    return f;
+}
+
+// One BVH node visit (near-first): descend into the nearer hit child, push
+// the farther one with its entry distance.
+__device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, D3 inv, double tmin,
+                                               double c, Stack& stk, uint32_t& sp) {
+    const float4* np = reinterpret_cast<const float4*>(S.nodes + idx);
+    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
+    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
+    const float lo1[3] = {q1.z, q1.w, q2.x}, hi1[3] = {q2.y, q2.z, q2.w};
+    const uint32_t c0 = __float_as_uint(q3.x), c1 = __float_as_uint(q3.y);
+    double e0, e1;
+    const bool h0 = slab2(lo0, hi0, r, inv, tmin, c, e0);
+    const bool h1 = c1 != REF_NONE && slab2(lo1, hi1, r, inv, tmin, c, e1);
+    if (h0 && h1) {
+        const bool first0 = e0 <= e1;
+        stk.push(sp++, first0 ? c1 : c0, f32_down(first0 ? e1 : e0));
+        return first0 ? c0 : c1;
+    }
+    return h0 ? c0 : (h1 ? c1 : REF_NONE);
+}
+
+// Pops until an entry whose box can still hold a hit closer than c.
+__device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t sp0, double c) {
+    while (sp > sp0) {
+        --sp;
+        const uint2 e = stk.at(sp);
+        if ((double)__uint_as_float(e.y) <= c) return e.x;
+    }
+    return REF_NONE;
+}
+
+constexpr float NO_CULL = -__builtin_huge_valf();
+
+// Closest t of a medium boundary (no media inside, no records) -- the two
+// boundary.hit calls of volume.rs:44-48.
+__device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax, Stack& stk,
+                           uint32_t sp0, double& tbest) {
     Ray r = r0;
     D3 inv = inv_dir(r.d);
     double a = len2(r.d);
@@ -227,32 +287,24 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
     bool found = false;
     for (;;) {
         if (cur == REF_NONE) {
-            if (sp == sp0) break;
-            --sp;
-            cur = stk[sp * RT_BLOCK];
+            cur = pop(stk, sp, sp0, c);
+            if (cur == REF_NONE) break;
         }
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
         cur = REF_NONE;
+        double t;
         switch (kind) {
-            case K_BVH: {
-                const DNode n = S.nodes[idx];
-                if (slab(n, r, inv, tmin, c)) {
-                    if (n.right != REF_NONE) stk[(sp++) * RT_BLOCK] = n.right;
-                    cur = n.left;
-                }
-                break;
-            }
+            case K_BVH: cur = visit_node(S, idx, r, inv, tmin, c, stk, sp); break;
             case K_LIST: {
                 const uint32_t child = S.list_children[idx];
                 if (child != REF_NONE) {
-                    if (S.list_children[idx + 1] != REF_NONE) stk[(sp++) * RT_BLOCK] = make_ref(K_LIST, idx + 1);
+                    if (S.list_children[idx + 1] != REF_NONE) stk.push(sp++, make_ref(K_LIST, idx + 1), NO_CULL);
                     cur = child;
                 }
                 break;
             }
             case K_SPHERE: {
                 const double4 s = S.spheres[idx];
-                double t;
                 if (sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t)) {
                     c = t;
                     found = true;
@@ -261,7 +313,6 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             }
             case K_MSPHERE: {
                 const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
-                double t;
                 const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
                 if (sphere_t(cc, s.w, r, a, tmin, c, t)) {
                     c = t;
@@ -270,17 +321,15 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 break;
             }
             case K_QUAD:
-            case K_TRI: {
-                double t;
+            case K_TRI:
                 if (planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t)) {
                     c = t;
                     found = true;
                 }
                 break;
-            }
             case K_XFORM: {
                 const DXform& X = S.xforms[idx];
-                stk[(sp++) * RT_BLOCK] = make_ref(K_POPXF, 0);
+                stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
                 xfs[nxf++] = idx;
                 r = xf_ray(X, r);
                 inv = inv_dir(r.d);
@@ -303,9 +352,12 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
     return found;
 }
 
-// world.hit(r, [1e-8, inf)) (camera.rs:286) as a DFS with one running closest
-// t: left subtree before right with the right interval shrunk (bvh.rs:70-82).
-__device__ bool trace(const SceneView& S, const Ray& wr, uint32_t* stk, const Rng& rng, HitInfo& hit) {
+// world.hit(r, [1e-8, inf)) (camera.rs:286) as a depth-first walk with one
+// running closest t.  Lists are walked in order with the interval shrunk to
+// the best hit so far (hits.rs:34-46 tests every child with the full interval
+// and keeps the first minimum: the same closest hit up to exact t ties).
+template <bool FULL>
+__device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit) {
     const double tmin = 1e-8;
     Ray r = wr;
     D3 inv = inv_dir(r.d);
@@ -318,93 +370,87 @@ __device__ bool trace(const SceneView& S, const Ray& wr, uint32_t* stk, const Rn
     bool found = false;
     for (;;) {
         if (cur == REF_NONE) {
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * RT_BLOCK];
+            cur = pop(stk, sp, 0, c);
+            if (cur == REF_NONE) break;
         }
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
         const uint32_t this_ref = cur;
         cur = REF_NONE;
         double t;
         bool got = false;
-        switch (kind) {
-            case K_BVH: {
-                const DNode n = S.nodes[idx];
-                if (slab(n, r, inv, tmin, c)) {
-                    if (n.right != REF_NONE) stk[(sp++) * RT_BLOCK] = n.right;
-                    cur = n.left;
+        if (kind == K_BVH) {
+            cur = visit_node(S, idx, r, inv, tmin, c, stk, sp);
+        } else if (kind == K_SPHERE) {
+            const double4 s = S.spheres[idx];
+            got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t);
+        } else if (kind == K_LIST) {
+            const uint32_t child = S.list_children[idx];
+            if (child != REF_NONE) {
+                if (S.list_children[idx + 1] != REF_NONE) stk.push(sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+                cur = child;
+            }
+        } else if constexpr (FULL) {
+            switch (kind) {
+                case K_MSPHERE: {
+                    const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
+                    const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
+                    got = sphere_t(cc, s.w, r, a, tmin, c, t);
+                    break;
                 }
-                break;
-            }
-            case K_LIST: {
-                const uint32_t child = S.list_children[idx];
-                if (child != REF_NONE) {
-                    if (S.list_children[idx + 1] != REF_NONE) stk[(sp++) * RT_BLOCK] = make_ref(K_LIST, idx + 1);
-                    cur = child;
+                case K_QUAD:
+                case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t); break;
+                case K_XFORM: {
+                    const DXform& X = S.xforms[idx];
+                    stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
+                    xfs[nxf++] = idx;
+                    r = xf_ray(X, r);
+                    inv = inv_dir(r.d);
+                    a = len2(r.d);
+                    cur = X.child;
+                    break;
                 }
-                break;
+                case K_POPXF: {
+                    --nxf;
+                    r = wr;
+                    for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
+                    inv = inv_dir(r.d);
+                    a = len2(r.d);
+                    break;
+                }
+                case K_MEDIUM: {
+                    // volume.rs:37-73
+                    const DMedium M = S.media[idx];
+                    double t1, t2;
+                    const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
+                    if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, sp, t1)) break;
+                    if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, sp, t2)) break;
+                    if (t1 < tmin) t1 = tmin;
+                    if (t2 > c) t2 = c;
+                    if (t1 >= t2) break;
+                    if (t1 < 0.0) t1 = 0.0;
+                    const double ray_length = len(r.d);
+                    const double inside = (t2 - t1) * ray_length;
+                    const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
+                    if (hd > inside) break;
+                    t = t1 + hd / ray_length;  // volume.rs:65
+                    got = t <= c;
+                    break;
+                }
+                default: break;
             }
-            case K_SPHERE: {
-                const double4 s = S.spheres[idx];
-                got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t);
-                break;
-            }
-            case K_MSPHERE: {
-                const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
-                const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-                got = sphere_t(cc, s.w, r, a, tmin, c, t);
-                break;
-            }
-            case K_QUAD:
-            case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t); break;
-            case K_XFORM: {
-                const DXform& X = S.xforms[idx];
-                stk[(sp++) * RT_BLOCK] = make_ref(K_POPXF, 0);
-                xfs[nxf++] = idx;
-                r = xf_ray(X, r);
-                inv = inv_dir(r.d);
-                a = len2(r.d);
-                cur = X.child;
-                break;
-            }
-            case K_POPXF: {
-                --nxf;
-                r = wr;
-                for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
-                inv = inv_dir(r.d);
-                a = len2(r.d);
-                break;
-            }
-            case K_MEDIUM: {
-                // volume.rs:37-73
-                const DMedium M = S.media[idx];
-                double t1, t2;
-                const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
-                if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, sp, t1)) break;
-                if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, sp, t2)) break;
-                if (t1 < tmin) t1 = tmin;
-                if (t2 > c) t2 = c;
-                if (t1 >= t2) break;
-                if (t1 < 0.0) t1 = 0.0;
-                const double ray_length = len(r.d);
-                const double inside = (t2 - t1) * ray_length;
-                const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
-                if (hd > inside) break;
-                t = t1 + hd / ray_length;  // volume.rs:65
-                got = true;
-                break;
-            }
-            default: break;
         }
-        if (got && (t <= c)) {
+        if (got) {
             c = t;
             found = true;
             hit.t = t;
             hit.ref = this_ref;
-            hit.nxf = nxf;
-            for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
+            if constexpr (FULL) {
+                hit.nxf = nxf;
+                for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
+            }
         }
     }
+    if constexpr (!FULL) hit.nxf = 0;
     return found;
 }
 
@@ -418,19 +464,21 @@ struct Rec {
 
 // HitRecord::new (hit.rs:24-43) of the recorded closest hit, in the frame of
 // its innermost Transform, then carried out through the chain (shapes.rs:104-108).
-__device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, bool need_uv_any) {
+template <bool FULL>
+__device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h) {
     Ray r = wr;
-    for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf[k]], r);
+    if constexpr (FULL)
+        for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf[k]], r);
     const uint32_t kind = ref_kind(h.ref), idx = ref_index(h.ref);
     Rec rec;
     rec.u = 0.0;
     rec.v = 0.0;
     const D3 p = r.o + h.t * r.d;
     D3 outward;
-    if (kind == K_SPHERE || kind == K_MSPHERE) {
+    if (!FULL || kind == K_SPHERE || kind == K_MSPHERE) {
         D3 c;
         double radius;
-        if (kind == K_SPHERE) {
+        if (!FULL || kind == K_SPHERE) {
             const double4 s = S.spheres[idx];
             c = d3(s.x, s.y, s.z);
             radius = s.w;
@@ -442,7 +490,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
             rec.mat = S.msph_mat[idx];
         }
         outward = divs(p - c, radius);  // sphere.rs:99
-        if (need_uv_any && (S.materials[rec.mat].flags & MF_NEEDS_UV)) {
+        if (S.materials[rec.mat].flags & MF_NEEDS_UV) {
             // sphere.rs:53-61
             const double theta = acos(-outward.y);
             const double phi = atan2(-outward.z, outward.x) + PI;
@@ -464,12 +512,13 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     rec.front = dot(r.d, outward) < 0.0;
     rec.n = rec.front ? outward : -outward;
     rec.p = p;
-    for (int k = (int)h.nxf - 1; k >= 0; --k) {
-        const DXform& X = S.xforms[h.xf[k]];
-        rec.p = xf_out(X, rec.p);
-        bool ok;
-        rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
-    }
+    if constexpr (FULL)
+        for (int k = (int)h.nxf - 1; k >= 0; --k) {
+            const DXform& X = S.xforms[h.xf[k]];
+            rec.p = xf_out(X, rec.p);
+            bool ok;
+            rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
+        }
     return rec;
 }
 
@@ -482,8 +531,7 @@ __device__ double light_pdf_one(const SceneView& S, uint32_t ref, D3 o, D3 d) {
         const DPlanar& P = S.planars[idx];
         if (!planar_t(P, kind == K_TRI, r, 1e-8, __builtin_huge_val(), t)) return 0.0;
         const D3 n = d3(P.f[0], P.f[1], P.f[2]);
-        const double front = dot(d, n) < 0.0 ? 1.0 : -1.0;
-        const D3 rn = front * n;
+        const D3 rn = dot(d, n) < 0.0 ? n : -n;
         const double distance_squared = t * t * len2(d);
         const double cosine = fabs(dot(d, rn) / len(d));
         return distance_squared / (cosine * S.planar_area[idx]);
@@ -506,7 +554,7 @@ __device__ double light_pdf(const SceneView& S, D3 o, D3 d) {
     for (uint32_t i = ref_index(root); S.list_children[i] != REF_NONE; ++i, ++n) sum += light_pdf_one(S, S.list_children[i], o, d);
     return sum / (double)n;
 }
-__device__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21, 34-38
+__device__ __forceinline__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21, 34-38
     const D3 a = fabs(n.x) > 0.9 ? d3(0.0, 1.0, 0.0) : d3(1.0, 0.0, 0.0);
     const D3 u = unit(cross(n, a), ok);
     const D3 w = cross(u, n);
@@ -560,22 +608,198 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
 
+// ------------------------------------------------------------------ one ray_color level
+// camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
+// true when the path ends here (miss, no scatter, panic).
+template <bool FULL>
+__device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, Stack& stk,
+                                       bool& panic) {
+    uint32_t ovf = 0;
+    HitInfo h;
+    if (!trace<FULL>(S, ray, stk, rng, h)) {
+        // miss: Environment::value (environment.rs:14-24)
+        if (S.background_tex >= 0) {
+            bool ok;
+            const D3 p = unit(ray.d, ok);
+            if (!ok) panic = true;
+            double u = 0.0, v = 0.0;
+            if (FULL && S.textures[S.background_tex].needs_uv) {
+                const double theta = acos(-p.y);
+                const double phi = PI - atan2(-p.z, p.x);
+                u = phi / (2.0 * PI);
+                v = theta / PI;
+            }
+            L = L + beta * tex_value<FULL>(S, S.background_tex, u, v, p);
+        }
+        return true;
+    }
+    const Rec rec = make_record<FULL>(S, ray, h);
+    DMaterial M = S.materials[rec.mat];
+    if constexpr (FULL) {
+        // emitted (material.rs:30-33, 171-178, 262-266)
+        if (M.flags & MF_EMISSIVE) {
+            D3 em;
+            if (M.type == M_DIFFUSE_LIGHT) {
+                em = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+            } else {  // Mix of non-wrapping materials (flatten checks)
+                const DMaterial& A = S.materials[M.inner];
+                const DMaterial& B = S.materials[M.inner2];
+                const D3 ea = A.type == M_DIFFUSE_LIGHT ? tex_value<FULL>(S, A.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                const D3 eb = B.type == M_DIFFUSE_LIGHT ? tex_value<FULL>(S, B.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                em = ((1.0 - M.fuzz) * ea) + (M.fuzz * eb);
+            }
+            L = L + beta * em;
+        }
+        // wrappers: DiffuseLight(inner) scatters as inner (material.rs:180-185); Mix draws (254-260)
+        if (M.type == M_DIFFUSE_LIGHT) {
+            if (M.inner < 0) return true;
+            M = S.materials[M.inner];
+        }
+        if (M.type == M_MIX) {
+            M = S.materials[rng.next(ovf) > M.fuzz ? M.inner : M.inner2];
+            if (M.type == M_DIFFUSE_LIGHT) return true;
+        }
+    }
+    const D3 n = rec.n;
+    int pdf_kind = -1;  // 0 cosine, 1 sphere
+    D3 albedo = d3(0, 0, 0);
+    switch (M.type) {
+        case M_LAMBERTIAN:  // material.rs:60-65
+            albedo = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+            pdf_kind = 0;
+            break;
+        case M_EMPTY:  // material.rs:41-46
+            albedo = d3(0.75, 0.75, 0.75);
+            pdf_kind = 0;
+            break;
+        case M_METAL: {  // material.rs:82-95
+            bool ok1, ok2;
+            const D3 ud = unit(ray.d, ok1);
+            if (!ok1) return true;
+            const D3 rr = unit(reflect(ud, n), ok2);
+            if (!ok2) return true;
+            const D3 ruv = random_unit_vector(rng, ovf);
+            beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
+            ray = Ray{rec.p, rr + (M.fuzz * ruv), ray.time};
+            break;
+        }
+        case M_DIELECTRIC: {  // material.rs:117-143
+            const double ri = rec.front ? 1.0 / M.fuzz : M.fuzz;
+            bool ok;
+            const D3 ud = unit(ray.d, ok);
+            if (!ok) panic = true;
+            const double cos_theta = fmin(dot(-ud, n), 1.0);
+            const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+            bool do_reflect = ri * sin_theta > 1.0;
+            if (!do_reflect) {  // Schlick (material.rs:110-114); the draw only when refraction is possible
+                const double r0 = (1.0 - ri) / (1.0 + ri);
+                const double r0sq = r0 * r0;
+                const double x = 1.0 - cos_theta;
+                const double x2 = x * x;
+                do_reflect = r0sq + (1.0 - r0sq) * (x * (x2 * x2)) > rng.next(ovf);
+            }
+            D3 dir;
+            if (do_reflect) {
+                dir = reflect(ud, n);
+            } else {  // vec3.rs:345-354
+                const D3 perp = ri * (ud + cos_theta * n);
+                const double pl = sqrt(1.0 - len2(perp));
+                if (isnan(pl)) panic = true;
+                dir = perp + (-pl * n);
+            }
+            beta = beta * tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+            ray = Ray{rec.p, dir, ray.time};
+            break;
+        }
+        default:
+            if constexpr (FULL) {
+                if (M.type == M_ISOTROPIC) {  // material.rs:199-206
+                    albedo = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+                    pdf_kind = 1;
+                    break;
+                }
+                if (M.type == M_TRANSPARENT) {  // material.rs:211-217
+                    ray = Ray{rec.p, ray.d, ray.time};
+                    break;
+                }
+            }
+            return true;
+    }
+    if (pdf_kind >= 0) {
+        // PDF branch (camera.rs:297-316)
+        const bool use_lights = FULL && S.lights_root != REF_NONE;
+        bool from_material = true;
+        if (use_lights) from_material = rng.next(ovf) < 0.5;  // MixturePDF::generate (pdf.rs:113-119)
+        D3 dir;
+        bool ok = true;
+        if (from_material) {
+            if (!FULL || pdf_kind == 0) {  // CosinePDF::generate (pdf.rs:59-63), vec3.rs:333-343
+                const double r1 = rng.next(ovf), r2 = rng.next(ovf);
+                double sn, cs;
+                sincos(2.0 * PI * r1, &sn, &cs);
+                const double sr2 = sqrt(r2);
+                dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
+            } else {
+                dir = random_unit_vector(rng, ovf);
+            }
+        } else {
+            dir = light_random(S, rec.p, rng, ovf, ok);
+        }
+        if (!ok) panic = true;
+        // value (pdf.rs:22-28, 50-57, 101-111)
+        D3 f;
+        double pdf;
+        if (!FULL || pdf_kind == 0) {
+            bool okd;
+            const D3 ud = unit(dir, okd);
+            if (!okd) panic = true;
+            const double ct = dot(ud, n);
+            pdf = fmax(0.0, ct / PI);
+            const double cp = fmax(ct, 0.0);
+            f = divs(albedo * d3(cp, cp, cp), PI);
+        } else {
+            pdf = 1.0 / (4.0 * PI);
+            f = divs(albedo, 4.0 * PI);
+        }
+        if (use_lights) {
+            const double pdf1 = light_pdf(S, rec.p, dir);
+            if (isnan(pdf1)) panic = true;
+            if (pdf == 0.0 && pdf1 == 0.0) panic = true;
+            pdf = pdf * 0.5 + pdf1 * 0.5;
+        }
+        if (pdf == 0.0) panic = true;  // camera.rs:309
+        beta = beta * divs(f, pdf);
+        ray = Ray{rec.p, dir, ray.time};
+    }
+    if (ovf) panic = true;
+    return panic;
+}
+
 // ------------------------------------------------------------------ the kernel
-struct LaneStats {
-    uint32_t rays, panics;
+// Launch parameters live in device memory and are read where they are used
+// (scalar loads), not pinned in SGPRs for the life of the kernel.
+struct KParams {
+    SceneView S;
+    Frame F;
+    uint32_t* queue;
+    double* partial;
+    unsigned long long* stats;
 };
 
-__global__ void __launch_bounds__(RT_BLOCK) rt_path_kernel(SceneView S, Frame F, uint32_t* __restrict__ queue,
-                                                          double* __restrict__ partial,
-                                                          unsigned long long* __restrict__ stats) {
-    __shared__ uint32_t stack_lds[RT_STACK * RT_BLOCK];
-    uint32_t* stk = stack_lds + threadIdx.x;
+template <bool FULL>
+__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const KParams* P) {
+    const SceneView& S = P->S;
+    const Frame& F = P->F;
+    uint32_t* queue = P->queue;
+    constexpr int STACK = FULL ? RT_STACK_FULL : RT_STACK_BASIC;
+    __shared__ uint2 stack_lds[STACK * RT_BLOCK];
+    Stack stk{stack_lds + threadIdx.x};
     const uint32_t lane = __lane_id();
 
     Rng rng;
     rng.k0 = F.key0;
     rng.k1 = F.key1;
-    uint32_t item = 0xFFFFFFFFu, s_j = 0, px = 0, py = 0;
+    uint32_t item = 0, s_j = 0, px = 0, py = 0;
     bool need = true;
     bool in_path = false;
     Ray ray;
@@ -633,187 +857,10 @@ __global__ void __launch_bounds__(RT_BLOCK) rt_path_kernel(SceneView S, Frame F,
         }
 
         // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
-        bool end_path = false;
-        uint32_t ovf = 0;
-        bool panic = false;
         rng.begin(vertex);
         ++n_rays;
-        HitInfo h;
-        if (!trace(S, ray, stk, rng, h)) {
-            // miss: Environment::value (environment.rs:14-24)
-            if (S.background_tex >= 0) {
-                bool ok;
-                const D3 p = unit(ray.d, ok);
-                if (!ok) panic = true;
-                double u = 0.0, v = 0.0;
-                if (S.textures[S.background_tex].needs_uv) {
-                    const double theta = acos(-p.y);
-                    const double phi = PI - atan2(-p.z, p.x);
-                    u = phi / (2.0 * PI);
-                    v = theta / PI;
-                }
-                L = L + beta * tex_value(S, S.background_tex, u, v, p);
-            }
-            end_path = true;
-        } else {
-            const Rec rec = make_record(S, ray, h, true);
-            int mat = rec.mat;
-            DMaterial M = S.materials[mat];
-            // emitted (material.rs:30-33, 171-178, 262-266)
-            if (M.flags & MF_EMISSIVE) {
-                D3 em;
-                if (M.type == M_DIFFUSE_LIGHT) {
-                    em = tex_value(S, M.tex, rec.u, rec.v, rec.p);
-                    D3 inner = d3(0, 0, 0);
-                    if (M.inner >= 0 && S.materials[M.inner].type == M_DIFFUSE_LIGHT) {
-                        const DMaterial& I = S.materials[M.inner];
-                        inner = tex_value(S, I.tex, rec.u, rec.v, rec.p);
-                    }
-                    em = em + inner;
-                } else {  // Mix
-                    const DMaterial& A = S.materials[M.inner];
-                    const DMaterial& B = S.materials[M.inner2];
-                    const D3 ea = A.type == M_DIFFUSE_LIGHT ? tex_value(S, A.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
-                    const D3 eb = B.type == M_DIFFUSE_LIGHT ? tex_value(S, B.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
-                    em = ((1.0 - M.fuzz) * ea) + (M.fuzz * eb);
-                }
-                L = L + beta * em;
-            }
-            // resolve wrappers: DiffuseLight(inner) scatters as inner; Mix draws (material.rs:254-260)
-            if (M.type == M_DIFFUSE_LIGHT) {
-                if (M.inner < 0) {
-                    end_path = true;
-                } else {
-                    mat = M.inner;
-                    M = S.materials[mat];
-                }
-            }
-            if (!end_path && M.type == M_MIX) {
-                mat = rng.next(ovf) > M.fuzz ? M.inner : M.inner2;
-                M = S.materials[mat];
-                if (M.type == M_DIFFUSE_LIGHT) end_path = true;  // DiffuseLight without inner: None
-            }
-            if (!end_path) {
-                const D3 n = rec.n;
-                int pdf_kind = -1;  // 0 cosine, 1 sphere
-                D3 albedo;
-                switch (M.type) {
-                    case M_LAMBERTIAN:  // material.rs:60-65
-                        albedo = tex_value(S, M.tex, rec.u, rec.v, rec.p);
-                        pdf_kind = 0;
-                        break;
-                    case M_EMPTY:  // material.rs:41-46
-                        albedo = d3(0.75, 0.75, 0.75);
-                        pdf_kind = 0;
-                        break;
-                    case M_ISOTROPIC:  // material.rs:199-206
-                        albedo = tex_value(S, M.tex, rec.u, rec.v, rec.p);
-                        pdf_kind = 1;
-                        break;
-                    case M_METAL: {  // material.rs:82-95
-                        bool ok1, ok2;
-                        const D3 ud = unit(ray.d, ok1);
-                        if (!ok1) {
-                            end_path = true;
-                            break;
-                        }
-                        const D3 rr = unit(reflect(ud, n), ok2);
-                        if (!ok2) {
-                            end_path = true;
-                            break;
-                        }
-                        const D3 ruv = random_unit_vector(rng, ovf);
-                        const D3 dir = rr + (M.fuzz * ruv);
-                        beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
-                        ray = Ray{rec.p, dir, ray.time};
-                        break;
-                    }
-                    case M_DIELECTRIC: {  // material.rs:117-143
-                        const double ri = rec.front ? 1.0 / M.fuzz : M.fuzz;
-                        bool ok;
-                        const D3 ud = unit(ray.d, ok);
-                        if (!ok) panic = true;
-                        const double cos_theta = fmin(dot(-ud, n), 1.0);
-                        const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
-                        const bool cannot_refract = ri * sin_theta > 1.0;
-                        bool do_reflect = cannot_refract;
-                        if (!do_reflect) {
-                            const double r0 = (1.0 - ri) / (1.0 + ri);
-                            const double r0sq = r0 * r0;
-                            const double x = 1.0 - cos_theta;
-                            const double x2 = x * x;
-                            const double refl = r0sq + (1.0 - r0sq) * (x * (x2 * x2));
-                            do_reflect = refl > rng.next(ovf);
-                        }
-                        D3 dir;
-                        if (do_reflect) {
-                            dir = reflect(ud, n);
-                        } else {  // vec3.rs:345-354
-                            const double ct = fmin(dot(-ud, n), 1.0);
-                            const D3 perp = ri * (ud + ct * n);
-                            const double pl = sqrt(1.0 - len2(perp));
-                            if (isnan(pl)) panic = true;
-                            dir = perp + (-pl * n);
-                        }
-                        beta = beta * tex_value(S, M.tex, rec.u, rec.v, rec.p);
-                        ray = Ray{rec.p, dir, ray.time};
-                        break;
-                    }
-                    case M_TRANSPARENT:  // material.rs:211-217
-                        ray = Ray{rec.p, ray.d, ray.time};
-                        break;
-                    default: end_path = true; break;
-                }
-                if (pdf_kind >= 0 && !end_path) {
-                    // PDF branch (camera.rs:297-316)
-                    const bool use_lights = S.lights_root != REF_NONE;
-                    bool from_material = true;
-                    if (use_lights) from_material = rng.next(ovf) < 0.5;  // MixturePDF::generate (pdf.rs:113-119)
-                    D3 dir;
-                    bool ok = true;
-                    if (from_material) {
-                        if (pdf_kind == 0) {  // CosinePDF::generate (pdf.rs:59-63), vec3.rs:333-343
-                            const double r1 = rng.next(ovf), r2 = rng.next(ovf);
-                            const double phi = 2.0 * PI * r1;
-                            double sn, cs;
-                            sincos(phi, &sn, &cs);
-                            const double sr2 = sqrt(r2);
-                            dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
-                        } else {
-                            dir = random_unit_vector(rng, ovf);
-                        }
-                    } else {
-                        dir = light_random(S, rec.p, rng, ovf, ok);
-                    }
-                    if (!ok) panic = true;
-                    // value (pdf.rs:22-28, 50-57, 101-111)
-                    D3 f;
-                    double pdf0;
-                    if (pdf_kind == 0) {
-                        bool okd;
-                        const D3 ud = unit(dir, okd);
-                        if (!okd) panic = true;
-                        const double ct = dot(ud, n);
-                        pdf0 = fmax(0.0, ct / PI);
-                        f = divs(albedo * d3(fmax(ct, 0.0), fmax(ct, 0.0), fmax(ct, 0.0)), PI);
-                    } else {
-                        pdf0 = 1.0 / (4.0 * PI);
-                        f = divs(albedo, 4.0 * PI);
-                    }
-                    double pdf = pdf0;
-                    if (use_lights) {
-                        const double pdf1 = light_pdf(S, rec.p, dir);
-                        if (isnan(pdf1)) panic = true;
-                        if (pdf0 == 0.0 && pdf1 == 0.0) panic = true;
-                        pdf = pdf0 * 0.5 + pdf1 * 0.5;
-                    }
-                    if (pdf == 0.0) panic = true;  // camera.rs:309
-                    beta = beta * divs(f, pdf);
-                    ray = Ray{rec.p, dir, ray.time};
-                }
-            }
-        }
-        if (ovf) panic = true;
+        bool panic = false;
+        bool end_path = bounce<FULL>(S, ray, beta, L, rng, stk, panic);
         if (panic) {
             ++n_panics;
             end_path = true;
@@ -831,7 +878,7 @@ __global__ void __launch_bounds__(RT_BLOCK) rt_path_kernel(SceneView S, Frame F,
             in_path = false;
             ++s_j;
             if (s_j == F.S) {
-                double* dst = partial + (uint64_t)item * 3;
+                double* dst = P->partial + (uint64_t)item * 3;
                 dst[0] = acc.x;
                 dst[1] = acc.y;
                 dst[2] = acc.z;
@@ -839,12 +886,12 @@ __global__ void __launch_bounds__(RT_BLOCK) rt_path_kernel(SceneView S, Frame F,
             }
         }
     }
-    atomicAdd(&stats[0], (unsigned long long)n_rays);
-    if (n_panics) atomicAdd(&stats[1], (unsigned long long)n_panics);
+    atomicAdd(&P->stats[0], (unsigned long long)n_rays);
+    if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
 }
 
 // Sums the S stratum rows of each pixel in s_i order, * pixel_sample_scale,
-// to linear f32 (camera.rs:193) and optionally sRGB u8 (utils/color.rs:27-36).
+// to linear f32 (camera.rs:193).
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
                                                        double scale, float* __restrict__ out) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -864,10 +911,18 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
 }  // namespace rtk
 
 // ------------------------------------------------------------------ host launchers
+extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
+    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_PLANAR | rtk::F_MSPHERE | rtk::F_LIGHTS |
+                          rtk::F_TEXFULL | rtk::F_MATFULL;
+    return ((features & full) || stack_need > RT_STACK_BASIC) ? 1 : 0;
+}
+
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int grid) {
-    rtk::Frame F;
+                                       int tier, int grid, void* params_dev) {
+    rtk::KParams K;
+    K.S = *view;
+    rtk::Frame& F = K.F;
     F.W = fd->W;
     F.rows = fd->rows;
     F.row_offset = fd->row_offset;
@@ -886,19 +941,32 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.dv = rtk::D3{fd->dv[0], fd->dv[1], fd->dv[2]};
     F.disk_u = rtk::D3{fd->disk_u[0], fd->disk_u[1], fd->disk_u[2]};
     F.disk_v = rtk::D3{fd->disk_v[0], fd->disk_v[1], fd->disk_v[2]};
-    hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    K.queue = queue;
+    K.partial = partial;
+    K.stats = stats;
+    rtk::KParams* Pd = (rtk::KParams*)params_dev;
+    hipError_t e = hipMemcpyAsync(Pd, &K, sizeof K, hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;
-    if (fd->ev_start) hipEventRecord((hipEvent_t)fd->ev_start, stream);
-    hipLaunchKernelGGL(rtk::rt_path_kernel, dim3(grid), dim3(RT_BLOCK), 0, stream, *view, F, queue, partial, stats);
+    e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
+    if (tier == 0)
+        hipLaunchKernelGGL(rtk::rt_path_kernel<false>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
+    else
+        hipLaunchKernelGGL(rtk::rt_path_kernel<true>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (fd->ev_stop) hipEventRecord((hipEvent_t)fd->ev_stop, stream);
+    if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
                        fd->pixel_sample_scale, out);
     return hipGetLastError();
 }
 
-extern "C" int rtk_path_kernel_occupancy(int* blocks_per_cu) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel, RT_BLOCK, 0);
+extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
+
+extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
+    if (tier == 0)
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<false>, RT_BLOCK, 0);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<true>, RT_BLOCK, 0);
 }

@@ -40,12 +40,17 @@ __host__ __device__ inline uint32_t ref_kind(uint32_t r) { return r >> 28; }
 __host__ __device__ inline uint32_t ref_index(uint32_t r) { return r & 0x0FFFFFFFu; }
 constexpr uint32_t REF_NONE = 0u;
 
-// bvh.rs:5-9 -- AABB (aabb.rs:10-14) + left/right.  64 B.
+// BVH node (bvh.rs:5-9 re-laid out): the boxes of BOTH children live in the
+// parent, as f32 rounded outward (lo down, hi up), so one 64-B line per node
+// visit feeds two slab tests.  The slab arithmetic stays f64 on the widened
+// boxes (conservative: every hit the reference's exact-box test admits is
+// admitted here).  c1 may be REF_NONE (a BVH over one object, bvh.rs:25).
 struct alignas(16) DNode {
-    double lo[3];
-    double hi[3];
-    uint32_t left, right;  // right may be REF_NONE (bvh.rs:25)
+    float lo0[3], hi0[3];
+    float lo1[3], hi1[3];
+    uint32_t c0, c1;
 };
+static_assert(sizeof(DNode) == 64, "DNode must be one 64-B line");
 
 // Planar: quad.rs:17-27 / triangle.rs:16-26 hot fields, packed in 128 B:
 // f[0..3) unit normal, f[3] parm_d, f[4..7) anchor, f[7..10) u, f[10..13) v,
@@ -144,6 +149,18 @@ struct SceneView {
     uint32_t lights_root;  // REF_NONE = lights: None
     int32_t background_tex;  // -1 = black
     uint32_t stack_need;     // max traversal stack entries (host-computed)
+    uint32_t features;       // F_* of everything reachable from world/lights
+};
+
+// Scene features; the launcher picks the smallest kernel tier covering them.
+enum : uint32_t {
+    F_XFORM = 1u,
+    F_MEDIUM = 2u,
+    F_PLANAR = 4u,
+    F_MSPHERE = 8u,
+    F_LIGHTS = 16u,
+    F_TEXFULL = 32u,  // image / noise textures
+    F_MATFULL = 64u,  // DiffuseLight, Isotropic, Transparent, Mix
 };
 
 }  // namespace rtk

@@ -22,6 +22,7 @@ struct DeviceWorld {
     // frame work buffers (grow-only)
     uint32_t* queue = nullptr;
     unsigned long long* stats = nullptr;
+    void* params = nullptr;
     double* partial = nullptr;
     size_t partial_bytes = 0;
     float* out = nullptr;
@@ -32,7 +33,10 @@ struct DeviceWorld {
     uint64_t pending_samples = 0;
     double pending_flatten_ms = 0;
     std::chrono::steady_clock::time_point pending_t0;
-    int grid = 0;
+    int grid[2] = {0, 0};
+    int tier = 1;
+    int cus = 0;
+    bool reference_bvh = false;
     hipStream_t pending_stream = nullptr;
 };
 
@@ -41,6 +45,7 @@ void destroy_device_world(DeviceWorld* d) {
     if (d->blob) (void)hipFree(d->blob);
     if (d->queue) (void)hipFree(d->queue);
     if (d->stats) (void)hipFree(d->stats);
+    if (d->params) (void)hipFree(d->params);
     if (d->partial) (void)hipFree(d->partial);
     if (d->out) (void)hipFree(d->out);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
@@ -62,7 +67,7 @@ static size_t put(std::vector<char>& blob, const std::vector<T>& v) {
 
 // Checks there is a gfx950 device and binds the scene's device world to it,
 // flattening + uploading when (world, lights, background, scene) changed.
-static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, double& flatten_ms) {
+static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, bool reference_bvh, double& flatten_ms) {
     flatten_ms = 0;
     int dev = -1;
     hipError_t e = hipGetDevice(&dev);
@@ -83,22 +88,29 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, d
         s->dev = d;
         if ((e = hipMalloc(&d->queue, 256)) != hipSuccess) return hip_fail(e, "hipMalloc queue");
         if ((e = hipMalloc(&d->stats, 256)) != hipSuccess) return hip_fail(e, "hipMalloc stats");
+        if ((e = hipMalloc(&d->params, rtk_params_bytes())) != hipSuccess) return hip_fail(e, "hipMalloc params");
         if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
         if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        int bpc = 0;
-        if ((e = (hipError_t)rtk_path_kernel_occupancy(&bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
-        if (bpc < 1) bpc = 1;
-        d->grid = bpc * prop.multiProcessorCount;
+        for (int t = 0; t < 2; ++t) {
+            int bpc = 0;
+            if ((e = (hipError_t)rtk_path_kernel_occupancy(t, &bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
+            if (bpc < 1) bpc = 1;
+            d->grid[t] = bpc * prop.multiProcessorCount;
+        }
+        d->cus = prop.multiProcessorCount;
     }
-    if (d->blob && d->world == world && d->lights == lights && d->background == bg && d->generation == s->generation)
+    if (d->blob && d->world == world && d->lights == lights && d->background == bg && d->generation == s->generation &&
+        d->reference_bvh == reference_bvh)
         return RT_OK;
     auto t0 = std::chrono::steady_clock::now();
     HostWorld hw;
-    int32_t rc = flatten(s, world, lights, bg, hw);
+    int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     if (rc != RT_OK) return rc;
-    if (hw.stack_need > RT_STACK)
+    const int tier = rtk_tier_for(hw.features, hw.stack_need);
+    const uint32_t stack_cap = tier == 0 ? RT_STACK_BASIC : RT_STACK_FULL;
+    if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
-                                        std::to_string(RT_STACK));
+                                        std::to_string(stack_cap));
     std::vector<char> blob;
     size_t o_nodes = put(blob, hw.nodes), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
            o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
@@ -135,6 +147,9 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, d
     v.lights_root = hw.lights_root;
     v.background_tex = bg;
     v.stack_need = hw.stack_need;
+    v.features = hw.features;
+    d->tier = tier;
+    d->reference_bvh = reference_bvh;
     d->blob_bytes = blob.size();
     d->n_prims = hw.n_prims;
     d->world = world;
@@ -243,7 +258,8 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     if (cam->background_tex != -1 && (cam->background_tex < 0 || (size_t)cam->background_tex >= s->texs.size()))
         return set_error(RT_EHANDLE, "unknown background texture");
     double flatten_ms = 0;
-    if ((rc = prepare(s, world, lights, cam->background_tex, flatten_ms)) != RT_OK) return rc;
+    const bool reference_bvh = opts && (opts->flags & RT_FLAG_REFERENCE_BVH);
+    if ((rc = prepare(s, world, lights, cam->background_tex, reference_bvh, flatten_ms)) != RT_OK) return rc;
     DeviceWorld* d = s->dev;
     if ((rc = ensure_buffers(d, f, dev_out == nullptr)) != RT_OK) return rc;
     hipError_t e = hipMemsetAsync(d->stats, 0, 2 * sizeof(unsigned long long), stream);
@@ -255,7 +271,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     float* out = dev_out ? dev_out : d->out;
     const bool run = f.rows > 0 && f.max_depth > 0;
     if (run) {
-        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->grid);
+        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->tier, d->grid[d->tier], d->params);
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
     } else if (f.rows > 0) {
         // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)
@@ -303,6 +319,32 @@ int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_ca
     if (!out_dev) return set_error(RT_EINVAL, "null device output");
     try {
         return launch(s, world, lights, cam, opts, out_dev, opts ? (hipStream_t)opts->stream : nullptr);
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
+}
+
+int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg, uint32_t flags, rt_world_info* out) {
+    if (!s || !out) return set_error(RT_EINVAL, "null argument");
+    if (world < 0 || (size_t)world >= s->objs.size() || s->objs[world].hidden)
+        return set_error(RT_EHANDLE, "unknown world handle");
+    try {
+        HostWorld hw;
+        int32_t rc = flatten(s, world, lights, bg, (flags & RT_FLAG_REFERENCE_BVH) != 0, hw);
+        if (rc != RT_OK) return rc;
+        std::vector<char> blob;
+        put(blob, hw.nodes), put(blob, hw.spheres), put(blob, hw.sphere_mat), put(blob, hw.msph_center),
+            put(blob, hw.msph_dir), put(blob, hw.msph_mat), put(blob, hw.planars), put(blob, hw.planar_area),
+            put(blob, hw.planar_mat), put(blob, hw.list_children), put(blob, hw.xforms), put(blob, hw.media),
+            put(blob, hw.materials), put(blob, hw.textures), put(blob, hw.texels), put(blob, hw.perlin);
+        out->device_bytes = blob.size();
+        out->bvh_nodes = (uint32_t)hw.nodes.size();
+        out->primitives = (uint32_t)hw.n_prims;
+        out->bvh_leaves = (uint32_t)hw.n_bvh_leaves;
+        out->stack_need = hw.stack_need;
+        out->kernel_tier = (uint32_t)rtk_tier_for(hw.features, hw.stack_need);
+        out->features = hw.features;
+        return RT_OK;
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }

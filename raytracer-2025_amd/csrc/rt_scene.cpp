@@ -108,12 +108,34 @@ static int bvh_from_vec(rt_scene* s, std::vector<int> objects) {
 
 // ------------------------------------------------------------------ flatten
 namespace {
+
+float round_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+float round_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+double half_area(const Box3& b) {
+    double dx = std::fmax(b.a[0].hi - b.a[0].lo, 0.0), dy = std::fmax(b.a[1].hi - b.a[1].lo, 0.0),
+           dz = std::fmax(b.a[2].hi - b.a[2].lo, 0.0);
+    return dx * dy + dy * dz + dz * dx;
+}
+
+constexpr int MAX_XF_NESTING = 2;  // rt_kernel.hip MAX_XF
+
 struct Flattener {
     const rt_scene* s;
     HostWorld& out;
+    bool reference_bvh;
     std::unordered_map<int, std::pair<uint32_t, uint32_t>> memo;  // obj -> (ref, stack need)
+    std::unordered_map<int, Box3> tight_memo;
     std::string err;
     int32_t code = RT_OK;
+    static constexpr uint32_t REF_NONE_ = rtk::REF_NONE;
 
     uint32_t fail(int32_t c, const std::string& m) {
         if (code == RT_OK) {
@@ -122,11 +144,175 @@ struct Flattener {
         }
         return REF_NONE_;
     }
-    static constexpr uint32_t REF_NONE_ = rtk::REF_NONE;
 
-    // Returns (ref, need) where need = traversal-stack entries used below the
-    // entry that held this ref (see rt_kernel.hip traverse()).
-    std::pair<uint32_t, uint32_t> emit(int id, bool in_boundary) {
+    // Tight box of everything an object can report a hit in.  The reference
+    // boxes (kept in Obj::bbox for the reference topology) include the origin
+    // for Hittables built from Hittables::default() (hits.rs:9, aabb.rs:9); the
+    // SAH build uses these tight ones instead.
+    Box3 tight(int id) {
+        auto it = tight_memo.find(id);
+        if (it != tight_memo.end()) return it->second;
+        const Obj& o = s->objs[id];
+        Box3 b = o.bbox;
+        switch (o.kind) {
+            case O_LIST:
+                b = Box3::empty();
+                for (int c : o.children) b = b.unite(tight(c));
+                break;
+            case O_BVH:
+                b = Box3::empty();
+                if (o.left >= 0) b = b.unite(tight(o.left));
+                if (o.right >= 0) b = b.unite(tight(o.right));
+                break;
+            case O_XFORM: {
+                Box3 cb = tight(o.child);
+                const double INFD = std::numeric_limits<double>::infinity();
+                V3 mn(INFD, INFD, INFD), mx(-INFD, -INFD, -INFD);
+                for (int i = 0; i < 8; ++i) {
+                    V3 p(cb.a[0].lo, cb.a[1].lo, cb.a[2].lo);
+                    if (i & 4) p.x = cb.a[0].hi;
+                    if (i & 2) p.y = cb.a[1].hi;
+                    if (i & 1) p.z = cb.a[2].hi;
+                    V3 t = o.q.rotate(p * o.scale) + o.offset;
+                    mn = V3(std::fmin(mn.x, t.x), std::fmin(mn.y, t.y), std::fmin(mn.z, t.z));
+                    mx = V3(std::fmax(mx.x, t.x), std::fmax(mx.y, t.y), std::fmax(mx.z, t.z));
+                }
+                b = Box3::from_points(mn, mx);
+                break;
+            }
+            case O_MEDIUM: b = tight(o.child); break;
+            default: break;
+        }
+        tight_memo[id] = b;
+        return b;
+    }
+
+    void set_box(rtk::DNode& n, int which, const Box3& b) {
+        float* lo = which ? n.lo1 : n.lo0;
+        float* hi = which ? n.hi1 : n.hi0;
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = round_down(b.a[k].lo);
+            hi[k] = round_up(b.a[k].hi);
+        }
+    }
+
+    struct Item {
+        uint32_t ref, need;
+        Box3 box;
+        double c[3];
+    };
+
+    // Binned SAH (32 bins x 3 axes) over items[b, e); leaves hold one object,
+    // the parent carries each child's box.  Returns (ref, need).
+    std::pair<uint32_t, uint32_t> sah(std::vector<Item>& it, size_t b, size_t e) {
+        if (e - b == 1) return {it[b].ref, it[b].need};
+        size_t mid = b + (e - b) / 2;
+        double cmin[3], cmax[3];
+        for (int k = 0; k < 3; ++k) {
+            cmin[k] = std::numeric_limits<double>::infinity();
+            cmax[k] = -cmin[k];
+        }
+        for (size_t i = b; i < e; ++i)
+            for (int k = 0; k < 3; ++k) {
+                cmin[k] = std::fmin(cmin[k], it[i].c[k]);
+                cmax[k] = std::fmax(cmax[k], it[i].c[k]);
+            }
+        constexpr int NB = 32;
+        double best = std::numeric_limits<double>::infinity();
+        int best_axis = -1, best_bin = 0;
+        for (int k = 0; k < 3; ++k) {
+            double ext = cmax[k] - cmin[k];
+            if (!(ext > 0)) continue;
+            Box3 bb[NB];
+            size_t cnt[NB] = {};
+            for (auto& x : bb) x = Box3::empty();
+            for (size_t i = b; i < e; ++i) {
+                int bin = (int)((it[i].c[k] - cmin[k]) / ext * NB);
+                bin = bin < 0 ? 0 : (bin >= NB ? NB - 1 : bin);
+                bb[bin] = bb[bin].unite(it[i].box);
+                ++cnt[bin];
+            }
+            double right_area[NB];
+            size_t right_cnt[NB];
+            Box3 acc = Box3::empty();
+            size_t n = 0;
+            for (int i = NB - 1; i > 0; --i) {
+                acc = acc.unite(bb[i]);
+                n += cnt[i];
+                right_area[i] = half_area(acc);
+                right_cnt[i] = n;
+            }
+            acc = Box3::empty();
+            n = 0;
+            for (int i = 0; i < NB - 1; ++i) {
+                acc = acc.unite(bb[i]);
+                n += cnt[i];
+                if (n == 0 || right_cnt[i + 1] == 0) continue;
+                double cost = half_area(acc) * (double)n + right_area[i + 1] * (double)right_cnt[i + 1];
+                if (cost < best) {
+                    best = cost;
+                    best_axis = k;
+                    best_bin = i;
+                }
+            }
+        }
+        if (best_axis >= 0) {
+            const int k = best_axis;
+            const double ext = cmax[k] - cmin[k];
+            auto pivot = std::stable_partition(it.begin() + b, it.begin() + e, [&](const Item& x) {
+                int bin = (int)((x.c[k] - cmin[k]) / ext * NB);
+                bin = bin < 0 ? 0 : (bin >= NB ? NB - 1 : bin);
+                return bin <= best_bin;
+            });
+            mid = (size_t)(pivot - it.begin());
+            if (mid == b || mid == e) mid = b + (e - b) / 2;
+        }
+        uint32_t idx = (uint32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        auto L = sah(it, b, mid);
+        auto R = sah(it, mid, e);
+        Box3 bl = Box3::empty(), br = Box3::empty();
+        for (size_t i = b; i < mid; ++i) bl = bl.unite(it[i].box);
+        for (size_t i = mid; i < e; ++i) br = br.unite(it[i].box);
+        rtk::DNode& n = out.nodes[idx];
+        set_box(n, 0, bl);
+        set_box(n, 1, br);
+        n.c0 = L.first;
+        n.c1 = R.first;
+        // near-first: the far child waits on the stack while the near one is walked
+        return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
+    }
+
+    // Reference topology (bvh.rs:16-46) in the two-box node format.
+    std::pair<uint32_t, uint32_t> ref_bvh(int id, bool in_boundary, int xf_depth, bool root) {
+        const Obj& o = s->objs[id];
+        if (!root && (o.kind != O_BVH || !o.hidden)) return emit(id, in_boundary, xf_depth);
+        uint32_t idx = (uint32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        auto L = ref_bvh(o.left, in_boundary, xf_depth, false);
+        std::pair<uint32_t, uint32_t> R{REF_NONE_, 0};
+        if (o.right >= 0) R = ref_bvh(o.right, in_boundary, xf_depth, false);
+        rtk::DNode& n = out.nodes[idx];
+        set_box(n, 0, s->objs[o.left].bbox);
+        if (o.right >= 0) set_box(n, 1, s->objs[o.right].bbox);
+        n.c0 = L.first;
+        n.c1 = R.first;
+        return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
+    }
+
+    void collect_leaves(int id, std::vector<int>& leaves) {
+        const Obj& o = s->objs[id];
+        if (o.kind == O_BVH && (o.hidden || leaves.empty())) {
+            collect_leaves(o.left, leaves);
+            if (o.right >= 0) collect_leaves(o.right, leaves);
+        } else {
+            leaves.push_back(id);
+        }
+    }
+
+    // Returns (ref, need): need = traversal-stack entries used below the entry
+    // that held this ref (rt_kernel.hip trace()).
+    std::pair<uint32_t, uint32_t> emit(int id, bool in_boundary, int xf_depth) {
         auto it = memo.find(id);
         if (it != memo.end()) return it->second;
         const Obj& o = s->objs[id];
@@ -146,6 +332,7 @@ struct Flattener {
                 out.msph_dir.push_back(make_double4(o.cdir.x, o.cdir.y, o.cdir.z, 0.0));
                 out.msph_mat.push_back(o.mat);
                 r = {rtk::make_ref(rtk::K_MSPHERE, idx), 0};
+                out.features |= rtk::F_MSPHERE;
                 ++out.n_prims;
                 break;
             }
@@ -160,44 +347,63 @@ struct Flattener {
                 out.planar_area.push_back(o.area);
                 out.planar_mat.push_back(o.mat);
                 r = {rtk::make_ref(o.kind == O_QUAD ? rtk::K_QUAD : rtk::K_TRI, idx), 0};
+                out.features |= rtk::F_PLANAR;
                 ++out.n_prims;
                 break;
             }
             case O_LIST: {
                 std::vector<std::pair<uint32_t, uint32_t>> kids;
-                for (int c : o.children) kids.push_back(emit(c, in_boundary));
+                for (int c : o.children) kids.push_back(emit(c, in_boundary, xf_depth));
                 uint32_t start = (uint32_t)out.list_children.size();
                 for (auto& k : kids) out.list_children.push_back(k.first);
                 out.list_children.push_back(REF_NONE_);
-                // iterator form: popping (LIST,p) pushes (LIST,p+1) then child p
+                // iterator form: popping (LIST,p) pushes (LIST,p+1) then walks child p
                 uint32_t need = 0;
                 for (size_t i = 0; i < kids.size(); ++i) {
                     bool last = i + 1 == kids.size();
-                    uint32_t here = last ? std::max<uint32_t>(1, kids[i].second) : std::max<uint32_t>(2, 1 + kids[i].second);
-                    need = std::max(need, here);
+                    need = std::max(need, last ? kids[i].second : 1 + kids[i].second);
                 }
                 r = {rtk::make_ref(rtk::K_LIST, start), need};
                 break;
             }
             case O_BVH: {
-                uint32_t idx = (uint32_t)out.nodes.size();
-                out.nodes.emplace_back();
-                auto L = o.left >= 0 ? emit(o.left, in_boundary) : std::pair<uint32_t, uint32_t>{REF_NONE_, 0};
-                auto R = o.right >= 0 ? emit(o.right, in_boundary) : std::pair<uint32_t, uint32_t>{REF_NONE_, 0};
-                rtk::DNode& n = out.nodes[idx];
-                for (int k = 0; k < 3; ++k) {
-                    n.lo[k] = o.bbox.a[k].lo;
-                    n.hi[k] = o.bbox.a[k].hi;
+                if (reference_bvh) {
+                    r = ref_bvh(id, in_boundary, xf_depth, true);
+                    break;
                 }
-                n.left = L.first;
-                n.right = R.first;
-                uint32_t need = o.right >= 0 ? std::max<uint32_t>(2, std::max(1 + L.second, R.second))
-                                             : std::max<uint32_t>(1, L.second);
-                r = {rtk::make_ref(rtk::K_BVH, idx), need};
+                std::vector<int> leaves;
+                collect_leaves(id, leaves);
+                std::vector<Item> items;
+                items.reserve(leaves.size());
+                for (int l : leaves) {
+                    auto e = emit(l, in_boundary, xf_depth);
+                    Item x;
+                    x.ref = e.first;
+                    x.need = e.second;
+                    x.box = tight(l);
+                    for (int k = 0; k < 3; ++k) x.c[k] = 0.5 * (x.box.a[k].lo + x.box.a[k].hi);
+                    items.push_back(x);
+                }
+                out.n_bvh_leaves += items.size();
+                if (items.size() == 1) {
+                    // BVH over one object: a node with one child keeps the box test
+                    uint32_t idx = (uint32_t)out.nodes.size();
+                    out.nodes.emplace_back();
+                    rtk::DNode& n = out.nodes[idx];
+                    set_box(n, 0, items[0].box);
+                    set_box(n, 1, Box3::empty());
+                    n.c0 = items[0].ref;
+                    n.c1 = REF_NONE_;
+                    r = {rtk::make_ref(rtk::K_BVH, idx), std::max<uint32_t>(1, items[0].need)};
+                } else {
+                    r = sah(items, 0, items.size());
+                }
                 break;
             }
             case O_XFORM: {
-                auto C = emit(o.child, in_boundary);
+                if (xf_depth >= MAX_XF_NESTING)
+                    return {fail(RT_EUNSUPPORTED, "Transform nested deeper than 2 levels"), 0};
+                auto C = emit(o.child, in_boundary, xf_depth + 1);
                 uint32_t idx = (uint32_t)out.xforms.size();
                 rtk::DXform x{};
                 x.off[0] = o.offset.x; x.off[1] = o.offset.y; x.off[2] = o.offset.z;
@@ -206,12 +412,13 @@ struct Flattener {
                 quat_matrix(o.q.conj(), x.rinv);
                 x.child = C.first;
                 out.xforms.push_back(x);
-                r = {rtk::make_ref(rtk::K_XFORM, idx), std::max<uint32_t>(2, 1 + C.second)};
+                out.features |= rtk::F_XFORM;
+                r = {rtk::make_ref(rtk::K_XFORM, idx), 1 + C.second};
                 break;
             }
             case O_MEDIUM: {
                 if (in_boundary) return {fail(RT_EUNSUPPORTED, "ConstantMedium inside a medium boundary"), 0};
-                auto B = emit(o.child, true);
+                auto B = emit(o.child, true, xf_depth);
                 uint32_t idx = (uint32_t)out.media.size();
                 rtk::DMedium m{};
                 m.neg_inv_density = o.neg_inv_density;
@@ -219,7 +426,8 @@ struct Flattener {
                 m.phase_mat = o.phase_mat;
                 m.medium_id = o.medium_id;
                 out.media.push_back(m);
-                r = {rtk::make_ref(rtk::K_MEDIUM, idx), std::max<uint32_t>(1, B.second)};
+                out.features |= rtk::F_MEDIUM;
+                r = {rtk::make_ref(rtk::K_MEDIUM, idx), B.second};
                 break;
             }
         }
@@ -252,7 +460,8 @@ static int tex_needs_uv(const rt_scene* s, int t, int depth = 0) {
     return 0;
 }
 
-int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, HostWorld& out) {
+int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, bool reference_bvh,
+                HostWorld& out) {
     out = HostWorld();
     // textures (texture.rs) and materials (material.rs) keep their handle ids
     for (size_t i = 0; i < s->texs.size(); ++i) {
@@ -317,8 +526,8 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
     }
     if (background_tex >= (int32_t)s->texs.size()) return set_error(RT_EHANDLE, "unknown background texture");
 
-    Flattener F{s, out, {}, {}, RT_OK};
-    auto W = F.emit(world, false);
+    Flattener F{s, out, reference_bvh, {}, {}, {}, RT_OK};
+    auto W = F.emit(world, false, 0);
     if (F.code != RT_OK) return set_error(F.code, F.err);
     out.world_root = W.first;
     out.stack_need = 1 + W.second;
@@ -327,10 +536,17 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         if (!light_ok(s, lights, 0))
             return set_error(RT_EUNSUPPORTED,
                              "lights must be a Sphere/Quad/Triangle or a non-empty Hittables of them on the kernel path");
-        auto Lr = F.emit(lights, false);
+        auto Lr = F.emit(lights, false, 0);
         if (F.code != RT_OK) return set_error(F.code, F.err);
         out.lights_root = Lr.first;
+        out.features |= rtk::F_LIGHTS;
     }
+    for (const auto& t : out.textures)
+        if (t.type == rtk::T_IMAGE || t.type == rtk::T_NOISE) out.features |= rtk::F_TEXFULL;
+    for (const auto& m : out.materials)
+        if (m.type == rtk::M_DIFFUSE_LIGHT || m.type == rtk::M_ISOTROPIC || m.type == rtk::M_TRANSPARENT ||
+            m.type == rtk::M_MIX)
+            out.features |= rtk::F_MATFULL;
     if (out.list_children.empty()) out.list_children.push_back(rtk::REF_NONE);
     return RT_OK;
 }

@@ -2,10 +2,11 @@
 //
 // Objects mirror the reference constructors (shapes/*.rs, hits.rs, bvh.rs,
 // volume.rs) as tagged records instead of trait objects; their bounding boxes
-// and the BVH topology are computed exactly as the reference computes them
-// (aabb.rs, bvh.rs:16-46, shapes.rs:49-72), so the flattened BVH has the
-// reference's topology and boxes.  `flatten` turns one (world, lights) pair
-// into the device layout of rt_layout.h.
+// and the reference BVH topology are computed exactly as the reference does
+// (aabb.rs, bvh.rs:16-46, shapes.rs:49-72).  `flatten` turns one (world,
+// lights) pair into the device layout of rt_layout.h; by default it rebuilds
+// every BVH with a binned SAH over the same objects (tight boxes), keeping the
+// reference topology only on request (RT_FLAG_REFERENCE_BVH).
 #pragma once
 #include <cmath>
 #include <cstdint>
@@ -115,7 +116,9 @@ struct HostWorld {
     std::vector<rtk::DPerlin> perlin;
     uint32_t world_root = 0, lights_root = 0;
     uint32_t stack_need = 0;
+    uint32_t features = 0;
     size_t n_prims = 0;
+    size_t n_bvh_leaves = 0;
 };
 
 struct DeviceWorld;  // rt_render.hip
@@ -137,6 +140,9 @@ struct rt_scene {
 namespace rth {
 int32_t set_error(int32_t code, const std::string& msg);
 // Flattens (world, lights) of scene s; lights = -1 for None.  Returns RT_OK or an RT_E* code.
-int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, HostWorld& out);
+// reference_bvh: keep the reference's BVH topology (bvh.rs:16-46) instead of
+// the binned-SAH rebuild (closest-hit results agree up to exact t ties).
+int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, bool reference_bvh,
+                HostWorld& out);
 void destroy_device_world(DeviceWorld* d);
 }  // namespace rth

@@ -219,7 +219,7 @@ class Camera:
         """pixels x floor(sqrt(spp))^2 -- what camera.rs:183-192 traces."""
         return self.image_width * self.image_height * self.sqrt_spp ** 2
 
-    def render(self, world, lights=None, seed=1, row_offset=0, row_stride=1, threads=0, want_srgb=True):
+    def render(self, world, lights=None, seed=1, row_offset=0, row_stride=1, threads=0, want_srgb=True, flags=0):
         """Camera::render (camera.rs:161).  Returns (linear HxWx3 f32, srgb HxWx3 u8 or None, RtStats)."""
         scene = world.scene
         api = scene.api
@@ -230,6 +230,7 @@ class Camera:
         opts.row_offset = int(row_offset)
         opts.row_stride = int(row_stride)
         opts.threads = int(threads)
+        opts.flags = int(flags)
         rows = api.shard_rows(C.byref(cam), C.byref(opts))
         W = self.image_width
         lin = np.zeros((rows, W, 3), dtype=np.float32)

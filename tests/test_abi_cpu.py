@@ -29,7 +29,8 @@ def test_header_symbols_exported(product, capi):
 
 
 def test_oracle_implements_same_abi(oracle, capi):
-    missing = [m for m in oracle.missing if not m.startswith("orc_render_device")]
+    # device-side entry points (stream-ordered render, flattened-world info) have no CPU meaning
+    missing = [m for m in oracle.missing if not m.startswith(("orc_render_device", "orc_world_info"))]
     assert not missing, missing
 
 

@@ -146,3 +146,20 @@ def _list_of_one(scene):
     lst = scene.Hittables()
     lst.add(scene.Quad((0, 0, 0), (1, 0, 0), (0, 1, 0), scene.EmptyMaterial()))
     return lst
+
+
+@pytest.mark.parametrize("which", ["c2", "c5"])
+def test_sah_matches_reference_topology(gpu, rt, scenes, which):
+    """The SAH rebuild changes only which nodes are visited: the image equals
+    the one rendered on the reference BVH topology (bvh.rs:16-46) up to exact
+    ties in t."""
+    scene = rt.Scene(gpu)
+    if which == "c2":
+        world, lights, cam = scenes.random_spheres(scene, 96, 9)
+    else:
+        world, lights, cam = scenes.final_scene(scene, 96, 9, 40, aspect_ratio=16 / 9)
+    a, _, _ = cam.render(world, lights, seed=5, flags=0)
+    b, _, _ = cam.render(world, lights, seed=5, flags=1)
+    rmse = rmse_per_channel(a, b)
+    print("SAH vs reference topology RMSE", rmse)
+    assert np.all(rmse < 1e-6)
