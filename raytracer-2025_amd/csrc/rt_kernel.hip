@@ -139,23 +139,54 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
 }
 
 // ------------------------------------------------------------------ geometry tests
-// aabb.rs:62-78 slab test on a child box stored f32 (outward-rounded), f64
-// arithmetic; inv = 1/d per axis, computed once per ray (the same value the
-// reference computes per node).  Returns the entry distance in `entry`.
-__device__ __forceinline__ bool slab2(const float* lo, const float* hi, const Ray& r, D3 inv, double tmin,
-                                      double tmax, double& entry) {
-    double t0 = ((double)lo[0] - r.o.x) * inv.x, t1 = ((double)hi[0] - r.o.x) * inv.x;
-    double a = fmax(tmin, fmin(t0, t1)), b = fmin(tmax, fmax(t0, t1));
-    t0 = ((double)lo[1] - r.o.y) * inv.y;
-    t1 = ((double)hi[1] - r.o.y) * inv.y;
-    a = fmax(a, fmin(t0, t1));
-    b = fmin(b, fmax(t0, t1));
-    t0 = ((double)lo[2] - r.o.z) * inv.z;
-    t1 = ((double)hi[2] - r.o.z) * inv.z;
-    a = fmax(a, fmin(t0, t1));
-    b = fmin(b, fmax(t0, t1));
-    entry = a;
-    return a <= b;
+// aabb.rs:62-78 slab test, in f32, made conservative: whenever the
+// reference's f64 test on the exact box admits [tmin, c], this one does too.
+//  - boxes are stored rounded outward (flatten);
+//  - the origin's f32 rounding (and the rounding of o*idf) is absorbed by
+//    widening the slab by pad = 2^-22 |o| per axis in space (RayF::nlo/nhi);
+//  - the fma and 1/d roundings (relative, < 3u) by widening the t-interval
+//    by 2^-22 |t| (REL);
+//  - 1/d is clamped to |.| <= 2^60 so a zero direction component gives huge
+//    finite t (the reference's +-inf) instead of inf - inf = NaN.
+struct RayF {
+    float idf[3];  // 1/d
+    float nlo[3];  // -(o + pad) * idf  (lo planes moved outward)
+    float nhi[3];  // -(o - pad) * idf  (hi planes moved outward)
+};
+__device__ __forceinline__ RayF make_rayf(const Ray& r) {
+    RayF R;
+    const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double id = 1.0 / d[k];
+        float f = (float)id;
+        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, (float)id);
+        const float of = (float)o[k];
+        const float pad = fabsf(of) * 2.384185791015625e-07f + 1e-30f;
+        R.idf[k] = f;
+        R.nlo[k] = -((of + pad) * f);
+        R.nhi[k] = -((of - pad) * f);
+    }
+    return R;
+}
+__device__ __forceinline__ float f32_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) {
+        const uint32_t b = __float_as_uint(f);
+        f = (f > 0.0f) ? __uint_as_float(b + 1u) : (f == 0.0f ? 1.401298464e-45f : __uint_as_float(b - 1u));
+    }
+    return f;
+}
+__device__ __forceinline__ bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f,
+                                       float& entry) {
+    const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
+    const float tly = fmaf(lo[1], R.idf[1], R.nlo[1]), thy = fmaf(hi[1], R.idf[1], R.nhi[1]);
+    const float tlz = fmaf(lo[2], R.idf[2], R.nlo[2]), thz = fmaf(hi[2], R.idf[2], R.nhi[2]);
+    const float nr = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+    const float fr = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+    constexpr float REL = 2.384185791015625e-07f;  // 2^-22
+    entry = fmaxf(fmaf(-fabsf(nr), REL, nr), tmin_f);
+    return entry <= fminf(fmaf(fabsf(fr), REL, fr), c_f);
 }
 
 // sphere.rs:77-96 -- t of the accepted root, or false
@@ -211,7 +242,6 @@ __device__ __forceinline__ Ray xf_ray(const DXform& X, const Ray& r) {
     const D3 lt = xf_in(X, r.o + 1.0 * r.d);
     return Ray{lo, lt - lo, r.time};
 }
-__device__ __forceinline__ D3 inv_dir(D3 d) { return d3(1.0 / d.x, 1.0 / d.y, 1.0 / d.z); }
 
 constexpr int MAX_XF = 2;
 
@@ -240,32 +270,61 @@ __device__ __forceinline__ float f32_down(double x) {
     return f;
 }
 
-// One BVH node visit (near-first): descend into the nearer hit child, push
-// the farther one with its entry distance.
-__device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, D3 inv, double tmin,
-                                               double c, Stack& stk, uint32_t& sp) {
+// Closest-hit state of one traversal: t and its f32 upper bound.
+struct Closest {
+    double c;
+    float c_f;
+    __device__ __forceinline__ void set(double t) {
+        c = t;
+        c_f = f32_up(t);
+    }
+};
+
+// One BVH node visit: both child boxes in f32; children that are spheres are
+// tested right here (sphere.rs:77-108), the remaining hit children are walked
+// near-first with the farther one pushed with its entry distance.
+template <class OnHit>
+__device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
+                                               double a, double tmin, float tmin_f, Closest& cl, Stack& stk,
+                                               uint32_t& sp, OnHit&& on_hit) {
     const float4* np = reinterpret_cast<const float4*>(S.nodes + idx);
     const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
     const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
     const float lo1[3] = {q1.z, q1.w, q2.x}, hi1[3] = {q2.y, q2.z, q2.w};
     const uint32_t c0 = __float_as_uint(q3.x), c1 = __float_as_uint(q3.y);
-    double e0, e1;
-    const bool h0 = slab2(lo0, hi0, r, inv, tmin, c, e0);
-    const bool h1 = c1 != REF_NONE && slab2(lo1, hi1, r, inv, tmin, c, e1);
+    float e0, e1;
+    bool h0 = slab_f(lo0, hi0, rf, tmin_f, cl.c_f, e0);
+    bool h1 = c1 != REF_NONE && slab_f(lo1, hi1, rf, tmin_f, cl.c_f, e1);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t ch = k ? c1 : c0;
+        bool& hk = k ? h1 : h0;
+        if (hk && ref_kind(ch) == K_SPHERE) {
+            const double4 sp4 = S.spheres[ref_index(ch)];
+            double t;
+            if (sphere_t(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, a, tmin, cl.c, t)) {
+                cl.set(t);
+                on_hit(ch, t);
+            }
+            hk = false;
+        }
+    }
+    h0 = h0 && e0 <= cl.c_f;
+    h1 = h1 && e1 <= cl.c_f;
     if (h0 && h1) {
         const bool first0 = e0 <= e1;
-        stk.push(sp++, first0 ? c1 : c0, f32_down(first0 ? e1 : e0));
+        stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
         return first0 ? c0 : c1;
     }
     return h0 ? c0 : (h1 ? c1 : REF_NONE);
 }
 
 // Pops until an entry whose box can still hold a hit closer than c.
-__device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t sp0, double c) {
+__device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t sp0, float c_f) {
     while (sp > sp0) {
         --sp;
         const uint2 e = stk.at(sp);
-        if ((double)__uint_as_float(e.y) <= c) return e.x;
+        if (__uint_as_float(e.y) <= c_f) return e.x;
     }
     return REF_NONE;
 }
@@ -277,24 +336,27 @@ constexpr float NO_CULL = -__builtin_huge_valf();
 __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax, Stack& stk,
                            uint32_t sp0, double& tbest) {
     Ray r = r0;
-    D3 inv = inv_dir(r.d);
+    RayF rf = make_rayf(r);
     double a = len2(r.d);
     uint32_t xfs[MAX_XF];
     uint32_t nxf = 0;
     uint32_t sp = sp0;
     uint32_t cur = root;
-    double c = tmax;
+    const float tmin_f = f32_down(tmin);
+    Closest cl;
+    cl.set(tmax);
     bool found = false;
+    auto on_hit = [&](uint32_t, double) { found = true; };
     for (;;) {
         if (cur == REF_NONE) {
-            cur = pop(stk, sp, sp0, c);
+            cur = pop(stk, sp, sp0, cl.c_f);
             if (cur == REF_NONE) break;
         }
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
         cur = REF_NONE;
         double t;
         switch (kind) {
-            case K_BVH: cur = visit_node(S, idx, r, inv, tmin, c, stk, sp); break;
+            case K_BVH: cur = visit_node(S, idx, r, rf, a, tmin, tmin_f, cl, stk, sp, on_hit); break;
             case K_LIST: {
                 const uint32_t child = S.list_children[idx];
                 if (child != REF_NONE) {
@@ -305,8 +367,8 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             }
             case K_SPHERE: {
                 const double4 s = S.spheres[idx];
-                if (sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t)) {
-                    c = t;
+                if (sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, cl.c, t)) {
+                    cl.set(t);
                     found = true;
                 }
                 break;
@@ -314,16 +376,16 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             case K_MSPHERE: {
                 const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
                 const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-                if (sphere_t(cc, s.w, r, a, tmin, c, t)) {
-                    c = t;
+                if (sphere_t(cc, s.w, r, a, tmin, cl.c, t)) {
+                    cl.set(t);
                     found = true;
                 }
                 break;
             }
             case K_QUAD:
             case K_TRI:
-                if (planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t)) {
-                    c = t;
+                if (planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t)) {
+                    cl.set(t);
                     found = true;
                 }
                 break;
@@ -332,7 +394,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
                 xfs[nxf++] = idx;
                 r = xf_ray(X, r);
-                inv = inv_dir(r.d);
+                rf = make_rayf(r);
                 a = len2(r.d);
                 cur = X.child;
                 break;
@@ -341,14 +403,14 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 --nxf;
                 r = r0;
                 for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
-                inv = inv_dir(r.d);
+                rf = make_rayf(r);
                 a = len2(r.d);
                 break;
             }
             default: break;
         }
     }
-    tbest = c;
+    tbest = cl.c;
     return found;
 }
 
@@ -359,18 +421,30 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 template <bool FULL>
 __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit) {
     const double tmin = 1e-8;
+    const float tmin_f = f32_down(tmin);
     Ray r = wr;
-    D3 inv = inv_dir(r.d);
+    RayF rf = make_rayf(r);
     double a = len2(r.d);
     uint32_t xfs[MAX_XF];
     uint32_t nxf = 0;
     uint32_t sp = 0;
     uint32_t cur = S.world_root;
-    double c = __builtin_huge_val();
+    Closest cl;
+    cl.c = __builtin_huge_val();
+    cl.c_f = __builtin_huge_valf();
     bool found = false;
+    auto record = [&](uint32_t ref, double t) {
+        found = true;
+        hit.t = t;
+        hit.ref = ref;
+        if constexpr (FULL) {
+            hit.nxf = nxf;
+            for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
+        }
+    };
     for (;;) {
         if (cur == REF_NONE) {
-            cur = pop(stk, sp, 0, c);
+            cur = pop(stk, sp, 0, cl.c_f);
             if (cur == REF_NONE) break;
         }
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
@@ -379,10 +453,10 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
         double t;
         bool got = false;
         if (kind == K_BVH) {
-            cur = visit_node(S, idx, r, inv, tmin, c, stk, sp);
+            cur = visit_node(S, idx, r, rf, a, tmin, tmin_f, cl, stk, sp, record);
         } else if (kind == K_SPHERE) {
             const double4 s = S.spheres[idx];
-            got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, c, t);
+            got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, cl.c, t);
         } else if (kind == K_LIST) {
             const uint32_t child = S.list_children[idx];
             if (child != REF_NONE) {
@@ -394,17 +468,17 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
                 case K_MSPHERE: {
                     const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
                     const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-                    got = sphere_t(cc, s.w, r, a, tmin, c, t);
+                    got = sphere_t(cc, s.w, r, a, tmin, cl.c, t);
                     break;
                 }
                 case K_QUAD:
-                case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, c, t); break;
+                case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t); break;
                 case K_XFORM: {
                     const DXform& X = S.xforms[idx];
                     stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
                     xfs[nxf++] = idx;
                     r = xf_ray(X, r);
-                    inv = inv_dir(r.d);
+                    rf = make_rayf(r);
                     a = len2(r.d);
                     cur = X.child;
                     break;
@@ -413,7 +487,7 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
                     --nxf;
                     r = wr;
                     for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
-                    inv = inv_dir(r.d);
+                    rf = make_rayf(r);
                     a = len2(r.d);
                     break;
                 }
@@ -425,7 +499,7 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
                     if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, sp, t1)) break;
                     if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, sp, t2)) break;
                     if (t1 < tmin) t1 = tmin;
-                    if (t2 > c) t2 = c;
+                    if (t2 > cl.c) t2 = cl.c;
                     if (t1 >= t2) break;
                     if (t1 < 0.0) t1 = 0.0;
                     const double ray_length = len(r.d);
@@ -433,21 +507,15 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
                     const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
                     if (hd > inside) break;
                     t = t1 + hd / ray_length;  // volume.rs:65
-                    got = t <= c;
+                    got = t <= cl.c;
                     break;
                 }
                 default: break;
             }
         }
         if (got) {
-            c = t;
-            found = true;
-            hit.t = t;
-            hit.ref = this_ref;
-            if constexpr (FULL) {
-                hit.nxf = nxf;
-                for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
-            }
+            cl.set(t);
+            record(this_ref, t);
         }
     }
     if constexpr (!FULL) hit.nxf = 0;

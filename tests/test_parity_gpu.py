@@ -163,3 +163,22 @@ def test_sah_matches_reference_topology(gpu, rt, scenes, which):
     rmse = rmse_per_channel(a, b)
     print("SAH vs reference topology RMSE", rmse)
     assert np.all(rmse < 1e-6)
+
+
+@pytest.mark.parametrize("name", ["c1_64x36_s16_seed7", "c3_48x48_s16_seed7", "c5_64x36_s16_seed7"])
+def test_gpu_vs_golden_fixture(gpu, rt, name):
+    """GPU against the committed oracle frames (tests/golden/), no oracle at run time."""
+    import importlib
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    gen_golden = importlib.import_module("gen_golden")
+    build, seed = gen_golden.CASES[name]
+    scene = rt.Scene(gpu)
+    world, lights, cam = build(scene)
+    lin, _, st = cam.render(world, lights, seed=seed)
+    ref = np.load(os.path.join(ROOT, "tests", "golden", name + ".npy"))
+    rmse = rmse_per_channel(lin, ref)
+    print(name, "RMSE vs golden", rmse)
+    assert np.all(rmse < TOL)
