@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reference-bvh", action="store_true",
                     help="A/B only: keep the reference BVH topology instead of the SAH rebuild")
+    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) on GPU nodes; gloo only to rehearse ranks on one GPU")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-row-stride", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=16)
@@ -115,10 +116,14 @@ def main():
                   file=sys.stderr)
             sys.exit(2)
     distributed = world_size > 1
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    local_dev = local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     if distributed:
-        dist.init_process_group("nccl", device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.backend)
 
     pkg = importlib.import_module(PKG)
     rt = importlib.import_module(PKG + ".raytracer")
@@ -151,7 +156,11 @@ def main():
         api.check(api.render_device_wait(scene.s, ctypes.byref(st)))  # HIP events around the path kernel
         if record:
             kernel_ms.append(st.kernel_ms)
-        frame = pdist.gather_frame(out[:rows], H, W) if distributed else out
+        if distributed:
+            shard = out[:rows] if args.backend == "nccl" else out[:rows].cpu()
+            frame = pdist.gather_frame(shard, H, W)
+        else:
+            frame = out
         return frame, st
 
     for _ in range(args.warmup):
@@ -167,10 +176,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        rdev = device if args.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-        km = torch.tensor([sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device=device)
+        km = torch.tensor([sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device=rdev)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
         kernel_avg_ms = km.item()
     else:
