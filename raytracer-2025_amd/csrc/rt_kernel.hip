@@ -24,6 +24,22 @@
 
 namespace rtk {
 
+// Diagnostic build (-DRT_DIAG, librt_mi355x_diag.so only): per-wave cycle
+// stamps and per-lane work counters, summed into g_diag.  The product build
+// compiles all of it away.
+struct Diag {
+#ifdef RT_DIAG
+    unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0;
+    unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
+#endif
+};
+#ifdef RT_DIAG
+__device__ unsigned long long g_diag[16];
+#define RT_DIAG_ONLY(x) x
+#else
+#define RT_DIAG_ONLY(x)
+#endif
+
 struct Ray {
     D3 o, d;
     double time;
@@ -65,7 +81,7 @@ __device__ double perlin_noise(const DPerlin& P, D3 p) {
 __device__ void image_pixel(const SceneView& S, const DTexture& t, int64_t x, int64_t y, float out[4]) {
     x = x < 0 ? 0 : (x > t.a - 1 ? t.a - 1 : x);
     y = y < 0 ? 0 : (y > t.b - 1 ? t.b - 1 : y);
-    const float* px = S.texels + t.data + ((uint64_t)y * t.a + x) * 4;
+    const RT_GLOBAL float* px = S.texels + t.data + ((uint64_t)y * t.a + x) * 4;
     out[0] = px[0];
     out[1] = px[1];
     out[2] = px[2];
@@ -198,11 +214,20 @@ __device__ __forceinline__ bool sphere_t(D3 c, double radius, const Ray& r, doub
     const double disc = h * h - a * cc;
     if (disc < 0.0) return false;
     const double sq = sqrt(disc);
+#ifdef RT_AB_SPHERE_RCP
+    const double inva = 1.0 / a;  // A/B only: not the reference's rounding
+    double root = (h - sq) * inva;
+    if (!(root >= tmin && root <= tmax)) {
+        root = (h + sq) * inva;
+        if (!(root >= tmin && root <= tmax)) return false;
+    }
+#else
     double root = (h - sq) / a;
     if (!(root >= tmin && root <= tmax)) {
         root = (h + sq) / a;
         if (!(root >= tmin && root <= tmax)) return false;
     }
+#endif
     t = root;
     return true;
 }
@@ -287,7 +312,7 @@ template <class OnHit>
 __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
                                                double a, double tmin, float tmin_f, Closest& cl, Stack& stk,
                                                uint32_t& sp, OnHit&& on_hit) {
-    const float4* np = reinterpret_cast<const float4*>(S.nodes + idx);
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
     const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
     const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
     const float lo1[3] = {q1.z, q1.w, q2.x}, hi1[3] = {q2.y, q2.z, q2.w};
@@ -299,7 +324,11 @@ __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx,
     for (int k = 0; k < 2; ++k) {
         const uint32_t ch = k ? c1 : c0;
         bool& hk = k ? h1 : h0;
+#ifdef RT_AB_NO_INLINE_SPHERE
+        if (false) {
+#else
         if (hk && ref_kind(ch) == K_SPHERE) {
+#endif
             const double4 sp4 = S.spheres[ref_index(ch)];
             double t;
             if (sphere_t(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, a, tmin, cl.c, t)) {
@@ -419,7 +448,8 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
 // and keeps the first minimum: the same closest hit up to exact t ties).
 template <bool FULL>
-__device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit) {
+__device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit, Diag& dg) {
+    RT_DIAG_ONLY(unsigned long long it = 0;)
     const double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
     Ray r = wr;
@@ -452,6 +482,7 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
         cur = REF_NONE;
         double t;
         bool got = false;
+        RT_DIAG_ONLY(++it; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
         if (kind == K_BVH) {
             cur = visit_node(S, idx, r, rf, a, tmin, tmin_f, cl, stk, sp, record);
         } else if (kind == K_SPHERE) {
@@ -519,6 +550,15 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
         }
     }
     if constexpr (!FULL) hit.nxf = 0;
+#ifdef RT_DIAG
+    dg.lane_trace_iters += it;
+    unsigned long long m = it;
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off);
+        m = o > m ? o : m;
+    }
+    dg.wave_trace_iters += m;
+#endif
     return found;
 }
 
@@ -681,10 +721,13 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 // true when the path ends here (miss, no scatter, panic).
 template <bool FULL>
 __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, Stack& stk,
-                                       bool& panic) {
+                                       bool& panic, Diag& dg) {
     uint32_t ovf = 0;
     HitInfo h;
-    if (!trace<FULL>(S, ray, stk, rng, h)) {
+    RT_DIAG_ONLY(const unsigned long long t_tr0 = __builtin_amdgcn_s_memtime();)
+    const bool hit_any = trace<FULL>(S, ray, stk, rng, h, dg);
+    RT_DIAG_ONLY(const unsigned long long t_tr1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_tr1 - t_tr0;)
+    if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
         if (S.background_tex >= 0) {
             bool ok;
@@ -855,8 +898,9 @@ struct KParams {
 };
 
 template <bool FULL>
-__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const KParams* P) {
-    const SceneView& S = P->S;
+__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const KParams* __restrict__ P) {
+    // The params block is read-only for the launch: scalar loads, hoisted.
+    const SceneView S = P->S;
     const Frame& F = P->F;
     uint32_t* queue = P->queue;
     constexpr int STACK = FULL ? RT_STACK_FULL : RT_STACK_BASIC;
@@ -875,7 +919,9 @@ __global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const K
     uint32_t vertex = 0;
     uint32_t n_rays = 0, n_panics = 0;
 
+    Diag dg;
     for (;;) {
+        RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
         // ---- refill: wave-aggregated dequeue of stratum rows
         const unsigned long long mask = __ballot(need);
         if (mask) {
@@ -928,7 +974,10 @@ __global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const K
         rng.begin(vertex);
         ++n_rays;
         bool panic = false;
-        bool end_path = bounce<FULL>(S, ray, beta, L, rng, stk, panic);
+        RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;
+                     const unsigned long long trace_before = dg.cyc_trace;)
+        bool end_path = bounce<FULL>(S, ray, beta, L, rng, stk, panic, dg);
+        RT_DIAG_ONLY(dg.cyc_shade += (__builtin_amdgcn_s_memtime() - t_b0) - (dg.cyc_trace - trace_before);)
         if (panic) {
             ++n_panics;
             end_path = true;
@@ -954,6 +1003,20 @@ __global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const K
             }
         }
     }
+#ifdef RT_DIAG
+    // wave-uniform cycle counts: lane 0 of each wave; lane counters: every lane
+    if (lane == 0) {
+        atomicAdd(&g_diag[0], dg.cyc_refill);
+        atomicAdd(&g_diag[1], dg.cyc_trace);
+        atomicAdd(&g_diag[2], dg.cyc_shade);
+        atomicAdd(&g_diag[3], dg.wave_trace_iters);
+        atomicAdd(&g_diag[4], dg.main_iters);
+    }
+    atomicAdd(&g_diag[5], dg.lane_trace_iters);
+    atomicAdd(&g_diag[6], dg.node_visits);
+    atomicAdd(&g_diag[7], dg.sphere_tests);
+    atomicAdd(&g_diag[8], (unsigned long long)n_rays);
+#endif
     atomicAdd(&P->stats[0], (unsigned long long)n_rays);
     if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
 }
@@ -1032,6 +1095,17 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
 }
 
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
+
+#ifdef RT_DIAG
+extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_diag), sizeof(unsigned long long) * 16);
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_diag), z, sizeof z);
+    }
+    return (int)e;
+}
+#endif
 
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
     if (tier == 0)

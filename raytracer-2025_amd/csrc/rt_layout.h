@@ -20,6 +20,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Device code reads the world through global-address-space pointers so loads
+// are global_load (vmcnt only), never flat_load (which also holds lgkmcnt and
+// so serialises with the LDS traversal stack).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RT_GLOBAL __attribute__((address_space(1)))
+#else
+#define RT_GLOBAL
+#endif
+
 namespace rtk {
 
 enum RefKind : uint32_t {
@@ -129,22 +138,22 @@ struct alignas(16) DPerlin {
 
 // Everything the kernel reads about the world, as device pointers.
 struct SceneView {
-    const DNode* nodes;
-    const double4* spheres;        // {cx, cy, cz, r}
-    const int32_t* sphere_mat;
-    const double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}
-    const double4* msph_dir;       // {c2-c1, 0}
-    const int32_t* msph_mat;
-    const DPlanar* planars;        // quads then triangles share the record
-    const double* planar_area;
-    const int32_t* planar_mat;
-    const uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
-    const DXform* xforms;
-    const DMedium* media;
-    const DMaterial* materials;
-    const DTexture* textures;
-    const float* texels;
-    const DPerlin* perlin;
+    const RT_GLOBAL DNode* nodes;
+    const RT_GLOBAL double4* spheres;        // {cx, cy, cz, r}
+    const RT_GLOBAL int32_t* sphere_mat;
+    const RT_GLOBAL double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}
+    const RT_GLOBAL double4* msph_dir;       // {c2-c1, 0}
+    const RT_GLOBAL int32_t* msph_mat;
+    const RT_GLOBAL DPlanar* planars;        // quads then triangles share the record
+    const RT_GLOBAL double* planar_area;
+    const RT_GLOBAL int32_t* planar_mat;
+    const RT_GLOBAL uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
+    const RT_GLOBAL DXform* xforms;
+    const RT_GLOBAL DMedium* media;
+    const RT_GLOBAL DMaterial* materials;
+    const RT_GLOBAL DTexture* textures;
+    const RT_GLOBAL float* texels;
+    const RT_GLOBAL DPerlin* perlin;
     uint32_t world_root;
     uint32_t lights_root;  // REF_NONE = lights: None
     int32_t background_tex;  // -1 = black

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of kernel variants (raytracer-2025_amd/librt_ab_*.so, built
+by `make -C raytracer-2025_amd ab`) in one process on the C2 scene: each
+variant renders the same frame; path-kernel time from the library's HIP
+events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]"""
+import ctypes
+import glob
+import importlib
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+capi = importlib.import_module("raytracer-2025_amd.capi")
+rt = importlib.import_module("raytracer-2025_amd.raytracer")
+scenes = importlib.import_module("raytracer-2025_amd.scenes")
+
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+names = sys.argv[3:] or sorted(os.path.basename(p)[len("librt_ab_"):-3]
+                                for p in glob.glob(os.path.join(ROOT, "raytracer-2025_amd", "librt_ab_*.so")))
+torch.cuda.init()
+runs = {}
+for n in names:
+    api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", f"librt_ab_{n}.so")), "rt_")
+    scene = rt.Scene(api)
+    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)  # warm-up
+    runs[n] = (scene, world, lights, cam, lin)
+res = {n: [] for n in names}
+for _ in range(reps):
+    for n in names:
+        scene, world, lights, cam, ref = runs[n]
+        lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)
+        res[n].append(st.kernel_ms)
+base = runs[names[0]][4]
+out = {}
+for n in names:
+    d = (runs[n][4].astype("float64") - base).reshape(-1, 3)
+    out[n] = {"kernel_ms_min": min(res[n]), "kernel_ms": res[n], "rmse_vs_first": float((d ** 2).mean() ** 0.5),
+              "msamples_per_s": cam.traced_samples() / (min(res[n]) * 1e-3) / 1e6}
+print(json.dumps(out, indent=1))

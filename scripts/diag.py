@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Diagnostic run (GPU box): renders C2 with librt_mi355x_diag.so (in-kernel
+s_memtime stamps + lane work counters, -DRT_DIAG) and prints where the wave
+cycles go and how full the lanes are in the traversal loop.  Read the shares,
+not the absolute time (stamps cost cycles)."""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+import torch  # noqa: F401  (one HIP runtime: load torch first)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+capi = importlib.import_module("raytracer-2025_amd.capi")
+rt = importlib.import_module("raytracer-2025_amd.raytracer")
+scenes = importlib.import_module("raytracer-2025_amd.scenes")
+
+torch.cuda.init()
+lib = ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", "librt_mi355x_diag.so"))
+api = capi.Api(lib, "rt_")
+lib.rt_diag_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+scene = rt.Scene(api)
+world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
+buf = (ctypes.c_ulonglong * 16)()
+lib.rt_diag_counters(buf, 1)
+_, _, st = cam.render(world, lights, seed=1, want_srgb=False)
+lib.rt_diag_counters(buf, 0)
+c = list(buf)
+tot = c[0] + c[1] + c[2]
+out = {
+    "spp": spp,
+    "kernel_ms": st.kernel_ms,
+    "samples": st.samples,
+    "rays": st.rays,
+    "cycle_share": {"refill+camera": c[0] / tot, "trace": c[1] / tot, "shade": c[2] / tot},
+    "trace_lane_efficiency": c[5] / (64.0 * c[3]) if c[3] else None,
+    "trace_iters_per_ray": c[5] / c[8],
+    "wave_trace_iters_per_wave_bounce": c[3] / max(1, c[4]),
+    "node_visits_per_ray": c[6] / c[8],
+    "sphere_tests_per_ray(not inlined)": c[7] / c[8],
+    "raw": c[:9],
+}
+print(json.dumps(out, indent=1))
