@@ -305,37 +305,39 @@ struct Closest {
     }
 };
 
-// One BVH node visit: both child boxes in f32; children that are spheres are
-// tested right here (sphere.rs:77-108), the remaining hit children are walked
-// near-first with the farther one pushed with its entry distance.
+// One BVH node visit (one 80-B record): a sphere child is intersected right
+// here from the data in its slot (sphere.rs:77-108); other children get the
+// f32 slab test, and the hit ones are walked near-first with the farther one
+// pushed with its entry distance.
 template <class OnHit>
 __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
                                                double a, double tmin, float tmin_f, Closest& cl, Stack& stk,
                                                uint32_t& sp, OnHit&& on_hit) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
-    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3];
-    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
-    const float lo1[3] = {q1.z, q1.w, q2.x}, hi1[3] = {q2.y, q2.z, q2.w};
-    const uint32_t c0 = __float_as_uint(q3.x), c1 = __float_as_uint(q3.y);
-    float e0, e1;
-    bool h0 = slab_f(lo0, hi0, rf, tmin_f, cl.c_f, e0);
-    bool h1 = c1 != REF_NONE && slab_f(lo1, hi1, rf, tmin_f, cl.c_f, e1);
+    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
+    const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
+    bool h0 = false, h1 = false;
+    float e0 = 0.0f, e1 = 0.0f;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const uint32_t ch = k ? c1 : c0;
+        const float4 qa = k ? q2 : q0, qb = k ? q3 : q1;
         bool& hk = k ? h1 : h0;
-#ifdef RT_AB_NO_INLINE_SPHERE
-        if (false) {
-#else
-        if (hk && ref_kind(ch) == K_SPHERE) {
-#endif
-            const double4 sp4 = S.spheres[ref_index(ch)];
+        float& ek = k ? e1 : e0;
+        if (ch == REF_NONE) continue;
+        if (ref_kind(ch) == K_SPHERE) {
+            const double cx = __hiloint2double(__float_as_int(qa.y), __float_as_int(qa.x));
+            const double cy = __hiloint2double(__float_as_int(qa.w), __float_as_int(qa.z));
+            const double cz = __hiloint2double(__float_as_int(qb.y), __float_as_int(qb.x));
+            const double rr = __hiloint2double(__float_as_int(qb.w), __float_as_int(qb.z));
             double t;
-            if (sphere_t(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, a, tmin, cl.c, t)) {
+            if (sphere_t(d3(cx, cy, cz), rr, r, a, tmin, cl.c, t)) {
                 cl.set(t);
                 on_hit(ch, t);
             }
-            hk = false;
+        } else {
+            const float lo[3] = {qa.x, qa.y, qa.z}, hi[3] = {qa.w, qb.x, qb.y};
+            hk = slab_f(lo, hi, rf, tmin_f, cl.c_f, ek);
         }
     }
     h0 = h0 && e0 <= cl.c_f;
@@ -473,10 +475,20 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
         }
     };
     for (;;) {
+#ifdef RT_AB_FLAT_POP
+        if (cur == REF_NONE) {
+            if (sp == 0) break;
+            --sp;
+            const uint2 e = stk.at(sp);
+            if (!(__uint_as_float(e.y) <= cl.c_f)) continue;  // culled entry: one empty iteration
+            cur = e.x;
+        }
+#else
         if (cur == REF_NONE) {
             cur = pop(stk, sp, 0, cl.c_f);
             if (cur == REF_NONE) break;
         }
+#endif
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
         const uint32_t this_ref = cur;
         cur = REF_NONE;
@@ -887,6 +899,10 @@ __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D
 }
 
 // ------------------------------------------------------------------ the kernel
+#ifndef RT_BASIC_WAVES
+#define RT_BASIC_WAVES 4  // waves per SIMD the basic tier is register-allocated for
+#endif
+
 // Launch parameters live in device memory and are read where they are used
 // (scalar loads), not pinned in SGPRs for the life of the kernel.
 struct KParams {
@@ -898,7 +914,7 @@ struct KParams {
 };
 
 template <bool FULL>
-__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : 4) rt_path_kernel(const KParams* __restrict__ P) {
+__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : RT_BASIC_WAVES) rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
     const Frame& F = P->F;

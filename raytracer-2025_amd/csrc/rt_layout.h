@@ -49,17 +49,30 @@ __host__ __device__ inline uint32_t ref_kind(uint32_t r) { return r >> 28; }
 __host__ __device__ inline uint32_t ref_index(uint32_t r) { return r & 0x0FFFFFFFu; }
 constexpr uint32_t REF_NONE = 0u;
 
-// BVH node (bvh.rs:5-9 re-laid out): the boxes of BOTH children live in the
-// parent, as f32 rounded outward (lo down, hi up), so one 64-B line per node
-// visit feeds two slab tests.  The slab arithmetic stays f64 on the widened
-// boxes (conservative: every hit the reference's exact-box test admits is
-// admitted here).  c1 may be REF_NONE (a BVH over one object, bvh.rs:25).
-struct alignas(16) DNode {
-    float lo0[3], hi0[3];
-    float lo1[3], hi1[3];
-    uint32_t c0, c1;
+// BVH node (bvh.rs:5-9 re-laid out): the parent carries what is needed to
+// test each child, so one node visit is one 80-B record:
+//  - a child that is a sphere stores the sphere itself (f64 center, radius:
+//    the exact data Sphere::hit reads, sphere.rs:77-108), tested directly --
+//    no box test, no dependent load;
+//  - any other child stores its AABB as f32 rounded outward (lo down, hi up);
+//    the slab test is made conservative (rt_kernel.hip slab_f), so every hit
+//    the reference's exact-box f64 test admits is admitted.
+// c1 may be REF_NONE (a BVH over one object, bvh.rs:25).
+struct alignas(16) DNodeSlot {
+    union {
+        struct {
+            float lo[3], hi[3];
+            uint32_t pad[2];
+        } box;
+        double sphere[4];  // {cx, cy, cz, r}
+    };
 };
-static_assert(sizeof(DNode) == 64, "DNode must be one 64-B line");
+struct alignas(16) DNode {
+    DNodeSlot slot[2];
+    uint32_t c0, c1;
+    uint32_t pad[2];
+};
+static_assert(sizeof(DNode) == 80, "DNode must be 80 B (5 dwordx4)");
 
 // Planar: quad.rs:17-27 / triangle.rs:16-26 hot fields, packed in 128 B:
 // f[0..3) unit normal, f[3] parm_d, f[4..7) anchor, f[7..10) u, f[10..13) v,

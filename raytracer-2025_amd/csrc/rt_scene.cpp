@@ -132,6 +132,9 @@ struct Flattener {
     HostWorld& out;
     bool reference_bvh;
     std::unordered_map<int, std::pair<uint32_t, uint32_t>> memo;  // obj -> (ref, stack need)
+    // The lights list keeps its run even with one object: Hittables::random
+    // spends a draw on `choose` regardless (hits.rs:69-75).
+    bool no_collapse = false;
     std::unordered_map<int, Box3> tight_memo;
     std::string err;
     int32_t code = RT_OK;
@@ -188,12 +191,25 @@ struct Flattener {
     }
 
     void set_box(rtk::DNode& n, int which, const Box3& b) {
-        float* lo = which ? n.lo1 : n.lo0;
-        float* hi = which ? n.hi1 : n.hi0;
+        auto& bx = n.slot[which].box;
         for (int k = 0; k < 3; ++k) {
-            lo[k] = round_down(b.a[k].lo);
-            hi[k] = round_up(b.a[k].hi);
+            bx.lo[k] = round_down(b.a[k].lo);
+            bx.hi[k] = round_up(b.a[k].hi);
         }
+        bx.pad[0] = bx.pad[1] = 0;
+    }
+    // child slot: the sphere itself for a sphere child, else its box
+    void set_child(rtk::DNode& n, int which, uint32_t ref, const Box3& b) {
+        if (rtk::ref_kind(ref) == rtk::K_SPHERE)
+        {
+            const double4 sp = out.spheres[rtk::ref_index(ref)];
+            n.slot[which].sphere[0] = sp.x;
+            n.slot[which].sphere[1] = sp.y;
+            n.slot[which].sphere[2] = sp.z;
+            n.slot[which].sphere[3] = sp.w;
+        }
+        else
+            set_box(n, which, b);
     }
 
     struct Item {
@@ -275,8 +291,8 @@ struct Flattener {
         for (size_t i = b; i < mid; ++i) bl = bl.unite(it[i].box);
         for (size_t i = mid; i < e; ++i) br = br.unite(it[i].box);
         rtk::DNode& n = out.nodes[idx];
-        set_box(n, 0, bl);
-        set_box(n, 1, br);
+        set_child(n, 0, L.first, bl);
+        set_child(n, 1, R.first, br);
         n.c0 = L.first;
         n.c1 = R.first;
         // near-first: the far child waits on the stack while the near one is walked
@@ -293,8 +309,9 @@ struct Flattener {
         std::pair<uint32_t, uint32_t> R{REF_NONE_, 0};
         if (o.right >= 0) R = ref_bvh(o.right, in_boundary, xf_depth, false);
         rtk::DNode& n = out.nodes[idx];
-        set_box(n, 0, s->objs[o.left].bbox);
-        if (o.right >= 0) set_box(n, 1, s->objs[o.right].bbox);
+        set_child(n, 0, L.first, s->objs[o.left].bbox);
+        if (o.right >= 0) set_child(n, 1, R.first, s->objs[o.right].bbox);
+        else set_box(n, 1, Box3::empty());
         n.c0 = L.first;
         n.c1 = R.first;
         return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
@@ -352,6 +369,10 @@ struct Flattener {
                 break;
             }
             case O_LIST: {
+                if (o.children.size() == 1 && !no_collapse) {  // world: min_by over one element is the element
+                    r = emit(o.children[0], in_boundary, xf_depth);
+                    break;
+                }
                 std::vector<std::pair<uint32_t, uint32_t>> kids;
                 for (int c : o.children) kids.push_back(emit(c, in_boundary, xf_depth));
                 uint32_t start = (uint32_t)out.list_children.size();
@@ -390,7 +411,7 @@ struct Flattener {
                     uint32_t idx = (uint32_t)out.nodes.size();
                     out.nodes.emplace_back();
                     rtk::DNode& n = out.nodes[idx];
-                    set_box(n, 0, items[0].box);
+                    set_child(n, 0, items[0].ref, items[0].box);
                     set_box(n, 1, Box3::empty());
                     n.c0 = items[0].ref;
                     n.c1 = REF_NONE_;
@@ -526,7 +547,7 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
     }
     if (background_tex >= (int32_t)s->texs.size()) return set_error(RT_EHANDLE, "unknown background texture");
 
-    Flattener F{s, out, reference_bvh, {}, {}, {}, RT_OK};
+    Flattener F{s, out, reference_bvh, {}, false, {}, {}, RT_OK};
     auto W = F.emit(world, false, 0);
     if (F.code != RT_OK) return set_error(F.code, F.err);
     out.world_root = W.first;
@@ -536,7 +557,10 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         if (!light_ok(s, lights, 0))
             return set_error(RT_EUNSUPPORTED,
                              "lights must be a Sphere/Quad/Triangle or a non-empty Hittables of them on the kernel path");
+        F.no_collapse = true;
+        F.memo.erase(lights);
         auto Lr = F.emit(lights, false, 0);
+        F.no_collapse = false;
         if (F.code != RT_OK) return set_error(F.code, F.err);
         out.lights_root = Lr.first;
         out.features |= rtk::F_LIGHTS;
