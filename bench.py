@@ -10,6 +10,7 @@ gathered to rank 0 over RCCL (N > 1).  Scaling is strong: the frame is fixed,
 ranks split it.  value = traced samples of all steps / max-over-ranks time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+  python bench.py --workload c4        # BASELINE configs[3]: 1M-triangle OBJ, 1920x1080, 256 spp
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 """
@@ -40,7 +41,20 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(threads, row_stride, spp):
+def build_workload(scenes, scene, workload, width, spp):
+    """(world, lights, cam, description) of a bench workload."""
+    if workload == "c2":
+        world, lights, cam = scenes.random_spheres(scene, width, spp)
+        return world, lights, cam, "C2: book-1 random spheres"
+    import tempfile
+    obj = os.path.join(tempfile.gettempdir(), "rt_terrain_707", "terrain.obj")
+    if not os.path.exists(obj):
+        scenes.write_terrain_obj(os.path.dirname(obj), 707)
+    world, lights, cam = scenes.obj_terrain(scene, obj, width, spp)
+    return world, lights, cam, "C4: synthetic 1M-triangle OBJ terrain (999 698 triangles, 2 models) + 2 spheres"
+
+
+def cpu_baseline(threads, row_stride, spp, workload="c2"):
     """The TEST-ONLY oracle (reference algorithm, f64, recursive ray_color,
     reference BVH topology) on the host cores: a bounded sample of the same
     C2 workload -- every `row_stride`-th row of the 1920x1080 frame at `spp`
@@ -53,7 +67,7 @@ def cpu_baseline(threads, row_stride, spp):
     scenes = importlib.import_module(PKG + ".scenes")
     api = capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
     scene = rt.Scene(api)
-    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    world, lights, cam, desc = build_workload(scenes, scene, workload, 1920, spp)
     c = cam.to_c()
     opts = capi.RtRenderOpts()
     api.render_opts_default(ctypes.byref(opts))
@@ -70,7 +84,7 @@ def cpu_baseline(threads, row_stride, spp):
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"C2 scene, every {row_stride}th row of 1920x1080 at {spp} spp ({cam.sqrt_spp**2} traced), "
+        "sample": f"{desc.split(':')[0]} scene, every {row_stride}th row of 1920x1080 at {spp} spp ({cam.sqrt_spp**2} traced), "
                   f"{st.samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
                   "(oracle/: reference-semantics C++ restatement, not the Rust binary)",
     }
@@ -93,7 +107,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
+                    help="c2 = BASELINE configs[1] (the headline metric); c4 = configs[3]")
+    ap.add_argument("--spp", type=int, default=None, help="default: 512 (c2), 256 (c4)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reference-bvh", action="store_true",
@@ -103,6 +119,8 @@ def main():
     ap.add_argument("--cpu-row-stride", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=16)
     args = ap.parse_args()
+    if args.spp is None:
+        args.spp = 512 if args.workload == "c2" else 256
 
     import torch
     import torch.distributed as dist
@@ -133,7 +151,7 @@ def main():
     api = pkg.load()
 
     scene = rt.Scene(api)
-    world, lights, cam = scenes.random_spheres(scene, args.width, args.spp)
+    world, lights, cam, desc = build_workload(scenes, scene, args.workload, args.width, args.spp)
     H, W = cam.image_height, cam.image_width
     c = cam.to_c()
     opts = capi.RtRenderOpts()
@@ -191,15 +209,18 @@ def main():
     value = frame_samples * args.steps / elapsed / 1e6
     if rank == 0:
         assert torch.isfinite(frame).all().item()
-        wc_path = os.path.join(ROOT, "bench_data", "work_counts_c2.json")
+        wc_path = os.path.join(ROOT, "bench_data", f"work_counts_{args.workload}.json")
         wc = json.load(open(wc_path))
         # one launch of the path kernel processes this rank's rows
         launch_samples = W * rows * sqrt_spp * sqrt_spp
         flops = wc["flops_per_sample"] * launch_samples
         achieved = flops / (kernel_avg_ms * 1e-3) / 1e12
-        traffic = load_pmc_traffic(os.path.join(ROOT, "profiles", "r01", "pmc_c2.json")) if world_size == 1 else None
+        traffic = (load_pmc_traffic(os.path.join(ROOT, "profiles", "r01", f"pmc_{args.workload}.json"))
+                   if world_size == 1 else None)
         line = {
-            "metric": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
+            "metric": ("Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)"
+                       if args.workload == "c2" else
+                       "Msamples/s (pixels x traced spp / s), synthetic 1M-triangle OBJ 1920x1080, 256 spp"),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world_size,
@@ -210,10 +231,12 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: book-1 random spheres from SplitMix64(2025) (raytracer-2025_amd/data), render RNG seed "
-                    + str(args.seed),
+            "data": ("synthetic: book-1 random spheres from SplitMix64(2025) (raytracer-2025_amd/data)"
+                     if args.workload == "c2" else
+                     "synthetic: displaced-grid terrain OBJ/MTL written by scenes.write_terrain_obj(707)")
+                    + ", render RNG seed " + str(args.seed),
             "config": {
-                "workload": f"C2: book-1 random spheres {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth 50, "
+                "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth 50, "
                             "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
                 "frame_samples": frame_samples,
                 "parallelism": f"row-shard x{world_size}",
@@ -230,11 +253,12 @@ def main():
                 "kernel_ms_avg": round(kernel_avg_ms, 3),
                 "flops_per_sample": round(wc["flops_per_sample"], 1),
                 "note": "algorithmic f64 FLOPs (reference algorithm on the reference BVH topology, "
-                        "bench_data/work_counts_c2.json) per launch / path-kernel time (HIP events on the render stream)",
+                        "bench_data/work_counts_<workload>.json) per launch / path-kernel time (HIP events on the render stream)",
             },
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, args.cpu_spp)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride if args.workload == "c2" else 8,
+                                                args.cpu_spp if args.workload == "c2" else 4, args.workload)
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()

@@ -108,6 +108,15 @@ int32_t rt_build_box(rt_scene* s, const double a[3], const double b[3], int32_t 
 int32_t rt_transform_new(rt_scene* s, int32_t object, const double* offset3, const double* quat_wxyz, const double* scale3);
 /* ConstantMedium::new_with_tex (volume.rs:23-33); moves `boundary` */
 int32_t rt_constant_medium_new(rt_scene* s, int32_t boundary, double density, int32_t tex);
+/* Wavefont::new (shapes/obj.rs:117-134) with the OBJ path given directly (the
+ * reference joins RTW_OBJS or ./assets, prefix and file name, obj.rs:86-115;
+ * MTL and map_* paths resolve against the OBJ's directory).  tobj
+ * GPU_LOAD_OPTIONS semantics; one BVH per loaded model, each triangle under a
+ * RemappedMaterial (vertex normals + texture coordinates, obj.rs:20-81).
+ * vanilla != 0: Metal / Dielectric from Pm / Tf (obj.rs:289-298); Disney
+ * materials, normal maps and image maps -> RT_EUNSUPPORTED.  Returns a
+ * Hittables object (possibly empty). */
+int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla);
 
 /* Quaternion::from_axis_angle / from_euler (utils/quaternion.rs:23-53), host helpers */
 int32_t rt_quat_from_axis_angle(const double axis[3], double angle_degrees, double out_wxyz[4]);
@@ -178,7 +187,7 @@ typedef struct rt_world_info {
     uint32_t primitives;      /* spheres + moving spheres + quads + triangles */
     uint32_t bvh_leaves;      /* objects under BVHs */
     uint32_t stack_need;      /* traversal-stack entries one lane needs */
-    uint32_t kernel_tier;     /* 0 = spheres/BVH/basic materials, 1 = full */
+    uint32_t kernel_tier;     /* 0 = spheres/BVH/basic materials, 1 = + quads/triangles/OBJ, 2 = full */
     uint32_t features;        /* F_* bits (rt_layout.h) */
 } rt_world_info;
 int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, uint32_t flags,

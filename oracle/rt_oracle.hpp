@@ -23,6 +23,7 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <map>
 #include <memory>
 #include <optional>
 #include <stdexcept>
@@ -616,6 +617,32 @@ struct Mix : Material {  // material.rs:220-268 (constant ratio form, Mix::new)
     }
 };
 
+// shapes/obj.rs:20-81 -- the per-triangle wrapper of an OBJ mesh (no normal
+// map: normal_tex = None).  remap_record replaces the normal by the normalised
+// barycentric mix of the vertex normals (not face-flipped) and (u, v) by the
+// interpolated texture coordinates; p, t, front_face are kept.
+struct RemappedMaterial : Material {
+    std::shared_ptr<Material> material;
+    Vec3 tex_ori, tex_u, tex_v;  // z = 0 (get_two_values, obj.rs:112-115)
+    Vec3 normal[3];
+    HitRecord remap_record(const HitRecord& rec) const {
+        Vec3 tex_coord = tex_ori + rec.u * tex_u + rec.v * tex_v;
+        Vec3 n = expect_unit((1.0 - rec.u - rec.v) * normal[0] + rec.u * normal[1] + rec.v * normal[2],
+                             "called `Option::unwrap()` on a `None` value (obj.rs:40)");
+        HitRecord h = rec;
+        h.normal = n;
+        h.u = tex_coord.e[0];
+        h.v = tex_coord.e[1];
+        return h;
+    }
+    std::optional<ScatterRecord> scatter(const Ray& r_in, const HitRecord& rec) const override {
+        return material->scatter(r_in, remap_record(rec));
+    }
+    Color emitted(const Ray& r_in, const HitRecord& rec) const override {
+        return material->emitted(r_in, remap_record(rec));
+    }
+};
+
 // ---------------------------------------------------------------- Hittables
 // src/hit.rs:46-60
 struct Hittable {
@@ -707,6 +734,28 @@ struct ConstantMedium : Hittable {  // src/volume.rs:16-78
 
 // ---------------------------------------------------------------- Camera
 // src/camera.rs:45-325
+// ---------------------------------------------------------------- OBJ (tobj restated, rt_oracle_obj.cpp)
+struct ObjMaterial {  // tobj::Material, the fields obj.rs:212-345 reads
+    std::string name;
+    bool has_diffuse = false, has_optical_density = false, has_dissolve = false;
+    Vec3 diffuse;
+    double optical_density = 0.0, dissolve = 1.0;
+    std::string diffuse_texture, normal_texture, dissolve_texture;
+    std::map<std::string, std::string> unknown_param;
+};
+struct ObjModel {  // tobj::Model / Mesh (single_index)
+    std::string name;
+    int material_id = -1;  // None
+    std::vector<double> positions, texcoords, normals;
+    std::vector<uint32_t> indices;
+};
+struct ObjFile {
+    std::vector<ObjModel> models;
+    std::vector<ObjMaterial> materials;
+    bool materials_ok = true;
+};
+ObjFile load_obj_file(const std::string& path);
+
 enum class ToonMap { None = 0, ACES = 1 };
 struct Camera {
     double aspect_ratio = 1.0;

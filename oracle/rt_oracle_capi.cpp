@@ -4,6 +4,8 @@
 // prefix `orc_` (liboracle.so), so tests can build one scene description on
 // both the gfx950 library and the oracle and compare the images.
 #include <cstdio>
+#include <fstream>
+#include <sstream>
 #include <mutex>
 #include <thread>
 
@@ -211,6 +213,111 @@ int32_t orc_constant_medium_new(rt_scene* s, int32_t boundary, double density, i
     if ((rc = s->check_obj(boundary)) != RT_OK) return rc;
     if (!s->tex_ok(tex)) return fail(RT_EHANDLE, "unknown texture");
     return s->add_obj(std::make_unique<ConstantMedium>(s->take(boundary), density, s->tex[tex], s->next_medium_id++));
+}
+
+// Wavefont::new (shapes/obj.rs:117-134), load_materials (212-345), load_object (137-194)
+int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
+    if (!s || !obj_path) return fail(RT_EINVAL, "null");
+    GUARD_BEGIN
+    ObjFile f = load_obj_file(obj_path);
+    const std::string path(obj_path);
+    const size_t slash = path.rfind('/');
+    const std::string prefix = slash == std::string::npos ? "." : path.substr(0, slash);
+    auto exists = [](const std::string& p) { return (bool)std::ifstream(p); };
+    auto parse_f64 = [](const std::string& v, double& out) {  // str::parse::<f64>
+        if (v.empty()) return false;
+        char* end = nullptr;
+        out = std::strtod(v.c_str(), &end);
+        return *end == 0;
+    };
+    auto param = [&](const ObjMaterial& m, const char* k, double def) {
+        auto it = m.unknown_param.find(k);
+        double x;
+        return (it != m.unknown_param.end() && parse_f64(it->second, x)) ? x : def;
+    };
+    auto values = [&](const std::string& v) {
+        std::vector<double> out;
+        std::istringstream is(v);
+        std::string w;
+        double x;
+        while (is >> w)
+            if (parse_f64(w, x)) out.push_back(x);
+        return out;
+    };
+    auto transparent = std::make_shared<Transparent>();
+    std::vector<std::shared_ptr<Material>> mats;
+    for (const ObjMaterial& m : f.materials) {
+        std::shared_ptr<Texture> base;
+        if (!m.diffuse_texture.empty()) {
+            if (exists(prefix + "/" + m.diffuse_texture))
+                return fail(RT_EUNSUPPORTED, "map_Kd images must be decoded by the caller");
+            base = std::make_shared<ImageTexture>();  // missing file -> cyan (texture.rs:167-169)
+        } else if (m.has_diffuse) {
+            base = std::make_shared<SolidColor>(m.diffuse);
+        } else {
+            throw Panic("The material should at least have one diffuse!");
+        }
+        if (!m.normal_texture.empty()) return fail(RT_EUNSUPPORTED, "normal maps are not supported");
+        const double roughness = param(m, "Pr", 0.5), metallic = param(m, "Pm", 0.0);
+        const double ior = m.has_optical_density ? m.optical_density : 1.45;
+        double spec_trans = 0.0;
+        auto tf = m.unknown_param.find("Tf");
+        if (tf != m.unknown_param.end()) {
+            std::vector<double> v = values(tf->second);
+            double sum = 0.0;
+            for (double x : v) sum += x;
+            spec_trans = sum / (double)v.size();
+        }
+        std::shared_ptr<Material> mat;
+        if (vanilla && metallic == 1.0)
+            mat = std::make_shared<Metal>(base->value(0.0, 0.0, Vec3(0, 0, 0)), roughness);
+        else if (vanilla && spec_trans == 1.0)
+            mat = std::make_shared<Dielectric>(base, ior);
+        else
+            return fail(RT_EUNSUPPORTED, "Disney BSDF materials are not supported");
+        auto ke = m.unknown_param.find("Ke");
+        if (ke != m.unknown_param.end()) {
+            std::vector<double> v = values(ke->second);
+            if (v.size() == 3) mat = std::make_shared<DiffuseLight>(std::make_shared<SolidColor>(Vec3(v[0], v[1], v[2])), mat);
+        }
+        if (m.unknown_param.count("map_Ke")) return fail(RT_EUNSUPPORTED, "map_Ke is not supported");
+        if (!m.dissolve_texture.empty()) return fail(RT_EUNSUPPORTED, "map_d is not supported");
+        if (m.has_dissolve && m.dissolve < 1.0) mat = std::make_shared<Mix>(transparent, mat, m.dissolve);
+        mats.push_back(mat);
+    }
+    auto objs = std::make_unique<Hittables>();
+    auto empty = std::make_shared<EmptyMaterial>();
+    const size_t n = std::min(f.models.size(), f.materials.size());  // objects.iter().zip(normals.iter())
+    for (size_t mi = 0; mi < n; ++mi) {
+        const ObjModel& o = f.models[mi];
+        std::vector<HittablePtr> v;
+        auto three = [](const std::vector<double>& a, uint32_t i) {
+            if ((size_t)i * 3 + 2 >= a.size()) throw Panic("index out of bounds (obj.rs:107-110)");
+            return Vec3(a[i * 3], a[i * 3 + 1], a[i * 3 + 2]);
+        };
+        auto two = [](const std::vector<double>& a, uint32_t i) {
+            if ((size_t)i * 2 + 1 >= a.size()) throw Panic("index out of bounds (obj.rs:112-115)");
+            return Vec3(a[i * 2], a[i * 2 + 1], 0.0);
+        };
+        for (size_t k = 0; k + 2 < o.indices.size(); k += 3) {
+            const uint32_t i0 = o.indices[k], i1 = o.indices[k + 1], i2 = o.indices[k + 2];
+            const Vec3 p1 = three(o.positions, i0), p2 = three(o.positions, i1), p3 = three(o.positions, i2);
+            const Vec3 t1 = two(o.texcoords, i0), t2 = two(o.texcoords, i1), t3 = two(o.texcoords, i2);
+            auto rm = std::make_shared<RemappedMaterial>();
+            rm->material = o.material_id >= 0 ? mats[o.material_id] : empty;
+            rm->tex_ori = t1;
+            rm->tex_u = t2 - t1;
+            rm->tex_v = t3 - t1;
+            rm->normal[0] = three(o.normals, i0);
+            rm->normal[1] = three(o.normals, i1);
+            rm->normal[2] = three(o.normals, i2);
+            auto tri = make_triangle(p1, p2 - p1, p3 - p1, rm);
+            if (tri) v.push_back(std::move(tri));
+        }
+        if (!v.empty()) objs->add(BVH::from_vec(std::move(v)));
+    }
+    return s->add_obj(std::move(objs));
+    GUARD_END
 }
 
 int32_t orc_quat_from_axis_angle(const double axis[3], double deg, double out[4]) {

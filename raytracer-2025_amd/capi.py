@@ -102,6 +102,7 @@ SIGNATURES = {
     "build_box": (_I, [_P, _DP, _DP, _I]),
     "transform_new": (_I, [_P, _I, _DP, _DP, _DP]),
     "constant_medium_new": (_I, [_P, _I, _D, _I]),
+    "wavefront_load": (_I, [_P, C.c_char_p, _I]),
     "quat_from_axis_angle": (_I, [_DP, _D, _DP]),
     "quat_from_euler": (None, [_D, _D, _D, _DP]),
     "camera_default": (None, [C.POINTER(RtCamera)]),

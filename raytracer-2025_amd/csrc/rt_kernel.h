@@ -9,7 +9,18 @@
 #define RT_BLOCK 256        // 4 waves of 64
 // traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
 #define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
+#define RT_STACK_MESH 32    // 64 KiB: 2 blocks per CU (deep triangle BVHs; VGPR-bound at 2 anyway)
 #define RT_STACK_FULL 32    // 64 KiB: 2 blocks per CU
+
+namespace rtk {
+// Kernel tiers: the launcher picks the smallest that covers the flattened world.
+//  BASIC: spheres / lists / BVH, Lambertian / Metal / Dielectric / Empty,
+//         solid / sky / checker textures, no lights (C1, C2);
+//  MESH:  BASIC + quads / triangles + OBJ RemappedMaterial (C4);
+//  FULL:  everything (transforms, media, moving spheres, lights, all materials
+//         and textures: C3, C5).
+enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2 };
+}  // namespace rtk
 
 // Camera::initilize results (camera.rs:204-245) for one shard.
 struct rtk_frame_desc {
@@ -23,9 +34,8 @@ struct rtk_frame_desc {
     void* ev_stop;
 };
 
-// tier 0: spheres / lists / BVH, Lambertian / Metal / Dielectric / Empty,
-// solid / sky / checker textures, no lights (C1, C2).  tier 1: everything.
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
+extern "C" uint32_t rtk_stack_entries(int tier);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, hipStream_t stream,
                                        int tier, int grid, void* params_dev);

@@ -449,8 +449,9 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
 // and keeps the first minimum: the same closest hit up to exact t ties).
-template <bool FULL>
+template <int TIER>
 __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit, Diag& dg) {
+    constexpr bool FULL = TIER == TIER_FULL;
     RT_DIAG_ONLY(unsigned long long it = 0;)
     const double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
@@ -506,6 +507,8 @@ __device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& 
                 if (S.list_children[idx + 1] != REF_NONE) stk.push(sp++, make_ref(K_LIST, idx + 1), NO_CULL);
                 cur = child;
             }
+        } else if constexpr (TIER == TIER_MESH) {
+            if (kind == K_TRI || kind == K_QUAD) got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t);
         } else if constexpr (FULL) {
             switch (kind) {
                 case K_MSPHERE: {
@@ -584,8 +587,9 @@ struct Rec {
 
 // HitRecord::new (hit.rs:24-43) of the recorded closest hit, in the frame of
 // its innermost Transform, then carried out through the chain (shapes.rs:104-108).
-template <bool FULL>
-__device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h) {
+template <int TIER>
+__device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, bool& panic) {
+    constexpr bool FULL = TIER == TIER_FULL, PLANAR = TIER >= TIER_MESH;
     Ray r = wr;
     if constexpr (FULL)
         for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf[k]], r);
@@ -595,7 +599,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h) 
     rec.v = 0.0;
     const D3 p = r.o + h.t * r.d;
     D3 outward;
-    if (!FULL || kind == K_SPHERE || kind == K_MSPHERE) {
+    if (!PLANAR || kind == K_SPHERE || kind == K_MSPHERE) {
         D3 c;
         double radius;
         if (!FULL || kind == K_SPHERE) {
@@ -639,6 +643,27 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h) 
             bool ok;
             rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
         }
+    if constexpr (PLANAR) {
+        // RemappedMaterial::remap_record (obj.rs:32-62), no normal map: applied to
+        // the record every material of an OBJ triangle sees (scatter and emitted)
+        if (kind == K_TRI) {
+            const int32_t ri = S.planar_remap[idx];
+            if (ri >= 0) {
+                const DRemap& R = S.remaps[ri];
+                const double u = rec.u, v = rec.v;
+                const double tu = (R.tex_ori[0] + u * R.tex_u[0]) + v * R.tex_v[0];
+                const double tv = (R.tex_ori[1] + u * R.tex_u[1]) + v * R.tex_v[1];
+                const double w0 = (1.0 - u) - v;
+                const D3 nm = ((w0 * d3(R.n[0], R.n[1], R.n[2])) + (u * d3(R.n[3], R.n[4], R.n[5]))) +
+                              (v * d3(R.n[6], R.n[7], R.n[8]));
+                bool ok;
+                rec.n = unit(nm, ok);
+                if (!ok) panic = true;  // .unwrap() (obj.rs:40)
+                rec.u = tu;
+                rec.v = tv;
+            }
+        }
+    }
     return rec;
 }
 
@@ -731,13 +756,14 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 // ------------------------------------------------------------------ one ray_color level
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
-template <bool FULL>
+template <int TIER>
 __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, Stack& stk,
                                        bool& panic, Diag& dg) {
+    constexpr bool FULL = TIER == TIER_FULL;
     uint32_t ovf = 0;
     HitInfo h;
     RT_DIAG_ONLY(const unsigned long long t_tr0 = __builtin_amdgcn_s_memtime();)
-    const bool hit_any = trace<FULL>(S, ray, stk, rng, h, dg);
+    const bool hit_any = trace<TIER>(S, ray, stk, rng, h, dg);
     RT_DIAG_ONLY(const unsigned long long t_tr1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_tr1 - t_tr0;)
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
@@ -756,7 +782,8 @@ __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D
         }
         return true;
     }
-    const Rec rec = make_record<FULL>(S, ray, h);
+    const Rec rec = make_record<TIER>(S, ray, h, panic);
+    if (panic) return true;
     DMaterial M = S.materials[rec.mat];
     if constexpr (FULL) {
         // emitted (material.rs:30-33, 171-178, 262-266)
@@ -902,6 +929,9 @@ __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D
 #ifndef RT_BASIC_WAVES
 #define RT_BASIC_WAVES 4  // waves per SIMD the basic tier is register-allocated for
 #endif
+#ifndef RT_MESH_WAVES
+#define RT_MESH_WAVES 2
+#endif
 
 // Launch parameters live in device memory and are read where they are used
 // (scalar loads), not pinned in SGPRs for the life of the kernel.
@@ -913,13 +943,14 @@ struct KParams {
     unsigned long long* stats;
 };
 
-template <bool FULL>
-__global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : RT_BASIC_WAVES) rt_path_kernel(const KParams* __restrict__ P) {
+template <int TIER>
+__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+    rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
     const Frame& F = P->F;
     uint32_t* queue = P->queue;
-    constexpr int STACK = FULL ? RT_STACK_FULL : RT_STACK_BASIC;
+    constexpr int STACK = TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
     __shared__ uint2 stack_lds[STACK * RT_BLOCK];
     Stack stk{stack_lds + threadIdx.x};
     const uint32_t lane = __lane_id();
@@ -992,7 +1023,7 @@ __global__ void __launch_bounds__(RT_BLOCK, FULL ? 2 : RT_BASIC_WAVES) rt_path_k
         bool panic = false;
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;
                      const unsigned long long trace_before = dg.cyc_trace;)
-        bool end_path = bounce<FULL>(S, ray, beta, L, rng, stk, panic, dg);
+        bool end_path = bounce<TIER>(S, ray, beta, L, rng, stk, panic, dg);
         RT_DIAG_ONLY(dg.cyc_shade += (__builtin_amdgcn_s_memtime() - t_b0) - (dg.cyc_trace - trace_before);)
         if (panic) {
             ++n_panics;
@@ -1059,9 +1090,14 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
 
 // ------------------------------------------------------------------ host launchers
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
-    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_PLANAR | rtk::F_MSPHERE | rtk::F_LIGHTS |
-                          rtk::F_TEXFULL | rtk::F_MATFULL;
-    return ((features & full) || stack_need > RT_STACK_BASIC) ? 1 : 0;
+    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL;
+    if ((features & full) || stack_need > RT_STACK_MESH) return rtk::TIER_FULL;
+    if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
+    return rtk::TIER_BASIC;
+}
+
+extern "C" uint32_t rtk_stack_entries(int tier) {
+    return tier == rtk::TIER_FULL ? RT_STACK_FULL : (tier == rtk::TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
 }
 
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
@@ -1097,10 +1133,12 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
-    if (tier == 0)
-        hipLaunchKernelGGL(rtk::rt_path_kernel<false>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
+    if (tier == rtk::TIER_BASIC)
+        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_BASIC>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
+    else if (tier == rtk::TIER_MESH)
+        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_MESH>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
     else
-        hipLaunchKernelGGL(rtk::rt_path_kernel<true>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
+        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_FULL>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
@@ -1124,7 +1162,9 @@ extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
 #endif
 
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
-    if (tier == 0)
-        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<false>, RT_BLOCK, 0);
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<true>, RT_BLOCK, 0);
+    if (tier == rtk::TIER_BASIC)
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_BASIC>, RT_BLOCK, 0);
+    if (tier == rtk::TIER_MESH)
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_MESH>, RT_BLOCK, 0);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_FULL>, RT_BLOCK, 0);
 }

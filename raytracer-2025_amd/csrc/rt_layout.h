@@ -81,6 +81,16 @@ struct alignas(16) DPlanar {
     double f[16];
 };
 
+// RemappedMaterial (shapes/obj.rs:20-29) of an OBJ triangle, applied to the
+// closest hit's record before shading: vertex normals n0..n2 (9 doubles),
+// tex_ori, tex_u, tex_v (2 each, z = 0 in the reference's Vec3).
+struct alignas(16) DRemap {
+    double n[9];
+    double tex_ori[2], tex_u[2], tex_v[2];
+    double pad;
+};
+static_assert(sizeof(DRemap) == 128, "DRemap must be 128 B");
+
 // Transform (shapes.rs:23-29).  Rotation kept as the quaternion the reference
 // uses plus its 3x3 matrix form (the kernel rotates with the matrix).
 struct alignas(16) DXform {
@@ -160,6 +170,8 @@ struct SceneView {
     const RT_GLOBAL DPlanar* planars;        // quads then triangles share the record
     const RT_GLOBAL double* planar_area;
     const RT_GLOBAL int32_t* planar_mat;
+    const RT_GLOBAL int32_t* planar_remap;   // index into remaps, -1 = plain Triangle/Quad
+    const RT_GLOBAL DRemap* remaps;
     const RT_GLOBAL uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
     const RT_GLOBAL DXform* xforms;
     const RT_GLOBAL DMedium* media;
@@ -183,6 +195,7 @@ enum : uint32_t {
     F_LIGHTS = 16u,
     F_TEXFULL = 32u,  // image / noise textures
     F_MATFULL = 64u,  // DiffuseLight, Isotropic, Transparent, Mix
+    F_REMAP = 128u,   // OBJ triangles with RemappedMaterial
 };
 
 }  // namespace rtk

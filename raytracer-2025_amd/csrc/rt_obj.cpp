@@ -1,0 +1,335 @@
+// rt_obj.cpp -- Wavefont::new (src/shapes/obj.rs:117-134) for the C ABI:
+// rt_wavefront_load.
+//
+// OBJ/MTL parsing restates what the reference gets from tobj 4.0.3 with
+// GPU_LOAD_OPTIONS (obj.rs:93, 104): single_index (one vertex per distinct
+// v/vt/vn triple, so positions/texcoords/normals share one index), triangulate
+// (fan 0,i,i+1), a new model at every `o`/`g` and at every `usemtl` that
+// changes the material of a model that already has faces.  tobj itself is not
+// in this image (parity unpinned for the parser).  Reference
+// behaviour kept on purpose:
+//  - models are zipped with the MTL materials (obj.rs:129): only the first
+//    min(#models, #materials) models are loaded;
+//  - every face vertex must carry vt and vn (obj.rs:148-158 index them
+//    unconditionally -> panic otherwise);
+//  - degenerate triangles are skipped (obj.rs:185-187), an empty model adds
+//    nothing (obj.rs:189-193);
+//  - each triangle's material is a RemappedMaterial (obj.rs:20-81): the
+//    shading normal is the normalised barycentric mix of the vertex normals and
+//    (u, v) become texture coordinates.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <unordered_map>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_scene.hpp"
+
+using namespace rth;
+
+namespace {
+
+struct MtlRec {
+    std::string name;
+    bool has_diffuse = false;
+    double diffuse[3] = {0, 0, 0};
+    std::string diffuse_texture, normal_texture, dissolve_texture;
+    bool has_ior = false, has_dissolve = false;
+    double ior = 1.45, dissolve = 1.0;
+    std::map<std::string, std::string> unknown;
+};
+
+std::string trim(const std::string& s) {
+    size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+    return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+
+bool parse_mtl(const std::string& path, std::vector<MtlRec>& out, std::string& err) {
+    std::ifstream f(path);
+    if (!f) {
+        err = "cannot open MTL " + path;
+        return false;
+    }
+    std::string line;
+    while (std::getline(f, line)) {
+        line = trim(line);
+        if (line.empty() || line[0] == '#') continue;
+        std::istringstream is(line);
+        std::string key;
+        is >> key;
+        std::string rest;
+        std::getline(is, rest);
+        rest = trim(rest);
+        if (key == "newmtl") {
+            out.emplace_back();
+            out.back().name = rest;
+            continue;
+        }
+        if (out.empty()) continue;
+        MtlRec& m = out.back();
+        std::istringstream vs(rest);
+        if (key == "Kd") {
+            vs >> m.diffuse[0] >> m.diffuse[1] >> m.diffuse[2];
+            m.has_diffuse = true;
+        } else if (key == "Ni") {
+            vs >> m.ior;
+            m.has_ior = true;
+        } else if (key == "d") {
+            vs >> m.dissolve;
+            m.has_dissolve = true;
+        } else if (key == "map_Kd") {
+            m.diffuse_texture = rest;
+        } else if (key == "map_Bump" || key == "map_bump" || key == "bump" || key == "norm") {
+            m.normal_texture = rest;
+        } else if (key == "map_d") {
+            m.dissolve_texture = rest;
+        } else if (key == "Ka" || key == "Ks" || key == "Ns" || key == "illum" || key == "map_Ka" || key == "map_Ks" ||
+                   key == "map_Ns") {
+            // known to tobj, unused by obj.rs
+        } else {
+            m.unknown[key] = rest;
+        }
+    }
+    return true;
+}
+
+// unknown_param.get(key).and_then(|s| s.parse::<f64>().ok()): the whole value must parse
+double param_or(const MtlRec& m, const char* key, double def) {
+    auto it = m.unknown.find(key);
+    if (it == m.unknown.end() || it->second.empty()) return def;
+    char* end = nullptr;
+    double v = std::strtod(it->second.c_str(), &end);
+    return *end == 0 ? v : def;
+}
+// split_whitespace().filter_map(|s| s.parse::<f64>().ok())
+std::vector<double> params(const MtlRec& m, const char* key) {
+    std::vector<double> v;
+    auto it = m.unknown.find(key);
+    if (it == m.unknown.end()) return v;
+    std::istringstream is(it->second);
+    std::string tok;
+    while (is >> tok) {
+        char* end = nullptr;
+        double x = std::strtod(tok.c_str(), &end);
+        if (*end == 0) v.push_back(x);
+    }
+    return v;
+}
+bool file_exists(const std::string& p) {
+    std::ifstream f(p);
+    return (bool)f;
+}
+
+struct Model {
+    std::string name;
+    int material_id = -1;
+    std::vector<int64_t> pos, tex, nrm;  // per single-index vertex: source indices
+    std::vector<uint32_t> indices;       // triangles
+    std::map<std::tuple<int64_t, int64_t, int64_t>, uint32_t> vmap;
+};
+
+}  // namespace
+
+extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
+    if (!s || !obj_path) return set_error(RT_EINVAL, "null argument");
+    try {
+        std::ifstream f(obj_path);
+        if (!f) return set_error(RT_EINVAL, std::string("cannot open OBJ ") + obj_path);
+        std::string path(obj_path);
+        std::string dir = path.find('/') == std::string::npos ? "." : path.substr(0, path.rfind('/'));
+        std::vector<double> P, T, N;  // v / vt / vn
+        std::vector<Model> models(1);
+        std::vector<MtlRec> mtls;
+        std::unordered_map<std::string, int> mtl_index;
+        bool mtl_failed = false;  // materials: Err(..) -> `if let Ok` skips them (obj.rs:124-126)
+        auto finish_model = [&](const std::string& next_name) {
+            Model& cur = models.back();
+            if (!cur.indices.empty()) {
+                Model nm;
+                nm.name = next_name;
+                nm.material_id = cur.material_id;
+                models.push_back(std::move(nm));
+            } else {
+                cur.name = next_name;
+            }
+        };
+        auto resolve = [](int64_t i, size_t n) -> int64_t { return i < 0 ? (int64_t)n + i : i - 1; };
+        std::string line;
+        while (std::getline(f, line)) {
+            size_t c = line.find('#');
+            if (c != std::string::npos) line.resize(c);
+            line = trim(line);
+            if (line.empty()) continue;
+            std::istringstream is(line);
+            std::string key;
+            is >> key;
+            if (key == "v") {
+                double x, y, z;
+                is >> x >> y >> z;
+                P.insert(P.end(), {x, y, z});
+            } else if (key == "vt") {
+                double u = 0, v = 0;
+                is >> u >> v;
+                T.insert(T.end(), {u, v});
+            } else if (key == "vn") {
+                double x, y, z;
+                is >> x >> y >> z;
+                N.insert(N.end(), {x, y, z});
+            } else if (key == "o" || key == "g") {
+                std::string rest;
+                std::getline(is, rest);
+                finish_model(trim(rest));
+            } else if (key == "mtllib") {
+                std::string rest;
+                std::getline(is, rest);
+                std::string err;
+                if (!parse_mtl(dir + "/" + trim(rest), mtls, err)) mtl_failed = true;
+                mtl_index.clear();
+                for (size_t i = 0; i < mtls.size(); ++i) mtl_index[mtls[i].name] = (int)i;
+            } else if (key == "usemtl") {
+                std::string rest;
+                std::getline(is, rest);
+                auto it = mtl_index.find(trim(rest));
+                int id = it == mtl_index.end() ? -1 : it->second;
+                Model& cur = models.back();
+                if (!cur.indices.empty() && cur.material_id != id) {
+                    Model nm;
+                    nm.name = cur.name;
+                    models.push_back(std::move(nm));
+                }
+                models.back().material_id = id;
+            } else if (key == "f") {
+                std::vector<uint32_t> face;
+                std::string tok;
+                Model& m = models.back();
+                while (is >> tok) {
+                    int64_t vi = 0, ti = INT64_MIN, ni = INT64_MIN;
+                    size_t a = tok.find('/');
+                    vi = resolve(std::stoll(tok.substr(0, a)), P.size() / 3);
+                    if (a != std::string::npos) {
+                        size_t b = tok.find('/', a + 1);
+                        std::string ts = tok.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
+                        if (!ts.empty()) ti = resolve(std::stoll(ts), T.size() / 2);
+                        if (b != std::string::npos && b + 1 < tok.size()) ni = resolve(std::stoll(tok.substr(b + 1)), N.size() / 3);
+                    }
+                    auto key3 = std::make_tuple(vi, ti, ni);
+                    auto it = m.vmap.find(key3);
+                    uint32_t idx;
+                    if (it == m.vmap.end()) {
+                        idx = (uint32_t)m.pos.size();
+                        m.vmap.emplace(key3, idx);
+                        m.pos.push_back(vi);
+                        m.tex.push_back(ti);
+                        m.nrm.push_back(ni);
+                    } else {
+                        idx = it->second;
+                    }
+                    face.push_back(idx);
+                }
+                for (size_t i = 1; i + 1 < face.size(); ++i) m.indices.insert(m.indices.end(), {face[0], face[i], face[i + 1]});
+            }
+        }
+        if (models.back().indices.empty() && models.size() > 1) models.pop_back();
+
+        if (mtl_failed) mtls.clear();
+        // load_materials (obj.rs:212-345)
+        std::vector<int32_t> mats;
+        for (const MtlRec& m : mtls) {
+            if (!m.normal_texture.empty())
+                return set_error(RT_EUNSUPPORTED, "normal maps (RemappedMaterial::normal_tex) are not on the kernel path");
+            int32_t base_tex;
+            if (!m.diffuse_texture.empty()) {
+                if (file_exists(dir + "/" + m.diffuse_texture))
+                    return set_error(RT_EUNSUPPORTED, "map_Kd images must be decoded by the caller (rt_tex_image)");
+                base_tex = rt_tex_image(s, 0, 0, nullptr, 0);  // missing file: cyan (texture.rs:167-169)
+            } else if (m.has_diffuse) {
+                base_tex = rt_tex_solid(s, m.diffuse);
+            } else {
+                return set_error(RT_EPANIC, "The material should at least have one diffuse!");
+            }
+            const double roughness = param_or(m, "Pr", 0.5), metallic = param_or(m, "Pm", 0.0);
+            const double ior = m.has_ior ? m.ior : 1.45;
+            std::vector<double> tf = params(m, "Tf");
+            double spec_trans = 0.0;
+            if (m.unknown.count("Tf")) {  // empty -> 0/0 = NaN, as the reference
+                double sum = 0;
+                for (double x : tf) sum += x;
+                spec_trans = sum / (double)tf.size();
+            }
+            int32_t mat;
+            if (vanilla && metallic == 1.0) {
+                const TexRec& t = s->texs[base_tex];
+                const double cyan[3] = {0.0, 1.0, 1.0};
+                mat = rt_mat_metal(s, t.type == rtk::T_SOLID ? t.color : cyan, roughness);
+            } else if (vanilla && spec_trans == 1.0) {
+                mat = rt_mat_dielectric(s, base_tex, ior);
+            } else {
+                return set_error(RT_EUNSUPPORTED, "Disney BSDF materials (obj.rs:299-311) are not on the kernel path");
+            }
+            std::vector<double> ke = params(m, "Ke");
+            if (ke.size() == 3) mat = rt_mat_diffuse_light(s, rt_tex_solid(s, ke.data()), mat);
+            if (m.unknown.count("map_Ke"))
+                return set_error(RT_EUNSUPPORTED, "map_Ke emission images are not on the kernel path");
+            if (!m.dissolve_texture.empty())
+                return set_error(RT_EUNSUPPORTED, "map_d dissolve images (Mix::from_image) are not on the kernel path");
+            if (m.has_dissolve && m.dissolve < 1.0) mat = rt_mat_mix(s, rt_mat_transparent(s), mat, m.dissolve);
+            if (mat < 0) return mat;
+            mats.push_back(mat);
+        }
+
+        int32_t objs = rt_hittables_new(s);
+        const int32_t empty = mats.empty() ? -1 : rt_mat_empty(s);
+        const size_t nload = std::min(models.size(), mtls.size());  // zip (obj.rs:129)
+        for (size_t mi = 0; mi < nload; ++mi) {
+            const Model& m = models[mi];
+            int32_t list = rt_hittables_new(s);
+            size_t added = 0;
+            const int32_t base = m.material_id >= 0 ? mats[m.material_id] : empty;
+            for (size_t k = 0; k + 2 < m.indices.size(); k += 3) {
+                uint32_t id[3] = {m.indices[k], m.indices[k + 1], m.indices[k + 2]};
+                V3 p[3], n[3];
+                double tc[3][2];
+                for (int j = 0; j < 3; ++j) {
+                    if (m.tex[id[j]] == INT64_MIN || m.nrm[id[j]] == INT64_MIN)
+                        return set_error(RT_EPANIC, "index out of bounds: face vertex without vt/vn (obj.rs:148-158)");
+                    const int64_t pi = m.pos[id[j]], ti = m.tex[id[j]], ni = m.nrm[id[j]];
+                    if (pi < 0 || (size_t)pi * 3 + 2 >= P.size() || ti < 0 || (size_t)ti * 2 + 1 >= T.size() || ni < 0 ||
+                        (size_t)ni * 3 + 2 >= N.size())
+                        return set_error(RT_EPANIC, "index out of bounds in OBJ face");
+                    p[j] = V3(&P[pi * 3]);
+                    n[j] = V3(&N[ni * 3]);
+                    tc[j][0] = T[ti * 2];
+                    tc[j][1] = T[ti * 2 + 1];
+                }
+                V3 wu = p[1] - p[0], wv = p[2] - p[0];
+                double a[3] = {p[0].x, p[0].y, p[0].z}, u[3] = {wu.x, wu.y, wu.z}, v[3] = {wv.x, wv.y, wv.z};
+                int32_t tri = rt_triangle(s, a, u, v, base);
+                if (tri == RT_EDEGENERATE) continue;
+                if (tri < 0) return tri;
+                Obj& o = s->objs[tri];
+                o.remap = true;
+                for (int j = 0; j < 3; ++j) o.rn[j] = n[j];
+                o.tex_ori[0] = tc[0][0];
+                o.tex_ori[1] = tc[0][1];
+                o.tex_u[0] = tc[1][0] - tc[0][0];
+                o.tex_u[1] = tc[1][1] - tc[0][1];
+                o.tex_v[0] = tc[2][0] - tc[0][0];
+                o.tex_v[1] = tc[2][1] - tc[0][1];
+                rt_hittables_add(s, list, tri);
+                ++added;
+            }
+            if (added) {
+                int32_t bvh = rt_bvh_new(s, list);  // BVH::from_vec (obj.rs:190)
+                if (bvh < 0) return bvh;
+                rt_hittables_add(s, objs, bvh);
+            }
+        }
+        return objs;
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    } catch (const std::exception& e) {
+        return set_error(RT_EINVAL, std::string("OBJ parse error: ") + e.what());
+    }
+}

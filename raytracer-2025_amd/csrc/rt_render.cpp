@@ -33,7 +33,7 @@ struct DeviceWorld {
     uint64_t pending_samples = 0;
     double pending_flatten_ms = 0;
     std::chrono::steady_clock::time_point pending_t0;
-    int grid[2] = {0, 0};
+    int grid[3] = {0, 0, 0};
     int tier = 1;
     int cus = 0;
     bool reference_bvh = false;
@@ -91,7 +91,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
         if ((e = hipMalloc(&d->params, rtk_params_bytes())) != hipSuccess) return hip_fail(e, "hipMalloc params");
         if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
         if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < 3; ++t) {
             int bpc = 0;
             if ((e = (hipError_t)rtk_path_kernel_occupancy(t, &bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
             if (bpc < 1) bpc = 1;
@@ -107,7 +107,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     if (rc != RT_OK) return rc;
     const int tier = rtk_tier_for(hw.features, hw.stack_need);
-    const uint32_t stack_cap = tier == 0 ? RT_STACK_BASIC : RT_STACK_FULL;
+    const uint32_t stack_cap = rtk_stack_entries(tier);
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
                                         std::to_string(stack_cap));
@@ -115,6 +115,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     size_t o_nodes = put(blob, hw.nodes), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
            o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
            o_pl = put(blob, hw.planars), o_pla = put(blob, hw.planar_area), o_plm = put(blob, hw.planar_mat),
+           o_plr = put(blob, hw.planar_remap), o_rm = put(blob, hw.remaps),
            o_lc = put(blob, hw.list_children), o_xf = put(blob, hw.xforms), o_md = put(blob, hw.media),
            o_mat = put(blob, hw.materials), o_tex = put(blob, hw.textures), o_tx = put(blob, hw.texels),
            o_per = put(blob, hw.perlin);
@@ -136,6 +137,8 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     v.planars = (const rtk::DPlanar*)(b + o_pl);
     v.planar_area = (const double*)(b + o_pla);
     v.planar_mat = (const int32_t*)(b + o_plm);
+    v.planar_remap = (const int32_t*)(b + o_plr);
+    v.remaps = (const rtk::DRemap*)(b + o_rm);
     v.list_children = (const uint32_t*)(b + o_lc);
     v.xforms = (const rtk::DXform*)(b + o_xf);
     v.media = (const rtk::DMedium*)(b + o_md);

@@ -363,6 +363,24 @@ struct Flattener {
                 out.planars.push_back(p);
                 out.planar_area.push_back(o.area);
                 out.planar_mat.push_back(o.mat);
+                if (o.remap) {
+                    rtk::DRemap rm{};
+                    for (int j = 0; j < 3; ++j) {
+                        rm.n[3 * j] = o.rn[j].x;
+                        rm.n[3 * j + 1] = o.rn[j].y;
+                        rm.n[3 * j + 2] = o.rn[j].z;
+                    }
+                    for (int j = 0; j < 2; ++j) {
+                        rm.tex_ori[j] = o.tex_ori[j];
+                        rm.tex_u[j] = o.tex_u[j];
+                        rm.tex_v[j] = o.tex_v[j];
+                    }
+                    out.planar_remap.push_back((int32_t)out.remaps.size());
+                    out.remaps.push_back(rm);
+                    out.features |= rtk::F_REMAP;
+                } else {
+                    out.planar_remap.push_back(-1);
+                }
                 r = {rtk::make_ref(o.kind == O_QUAD ? rtk::K_QUAD : rtk::K_TRI, idx), 0};
                 out.features |= rtk::F_PLANAR;
                 ++out.n_prims;
@@ -530,21 +548,6 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
                     if (sub >= 0) m.flags |= out.materials[sub].flags & (rtk::MF_NEEDS_UV | rtk::MF_EMISSIVE);
             }
         }
-    for (size_t i = 0; i < out.materials.size(); ++i) {
-        const rtk::DMaterial& m = out.materials[i];
-        if (m.type == rtk::M_MIX) {
-            for (int sub : {m.inner, m.inner2}) {
-                int st = out.materials[sub].type;
-                if (st == rtk::M_MIX || (st == rtk::M_DIFFUSE_LIGHT && out.materials[sub].inner >= 0))
-                    return set_error(RT_EUNSUPPORTED, "Mix of Mix / of DiffuseLight-with-material is not on the kernel path yet");
-            }
-        }
-        if (m.type == rtk::M_DIFFUSE_LIGHT && m.inner >= 0) {
-            int st = out.materials[m.inner].type;
-            if (st == rtk::M_MIX || st == rtk::M_DIFFUSE_LIGHT)
-                return set_error(RT_EUNSUPPORTED, "DiffuseLight wrapping Mix/DiffuseLight is not on the kernel path yet");
-        }
-    }
     if (background_tex >= (int32_t)s->texs.size()) return set_error(RT_EHANDLE, "unknown background texture");
 
     Flattener F{s, out, reference_bvh, {}, false, {}, {}, RT_OK};
@@ -565,12 +568,71 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         out.lights_root = Lr.first;
         out.features |= rtk::F_LIGHTS;
     }
-    for (const auto& t : out.textures)
-        if (t.type == rtk::T_IMAGE || t.type == rtk::T_NOISE) out.features |= rtk::F_TEXFULL;
-    for (const auto& m : out.materials)
+    // Materials and textures reachable from the emitted primitives and the
+    // background decide the kernel tier (an unused DiffuseLight in the scene
+    // must not force the full tier) and are the ones checked for support.
+    std::vector<char> mat_used(out.materials.size(), 0), tex_used(out.textures.size(), 0);
+    std::vector<int> work;
+    auto use_mat = [&](int m) {
+        if (m >= 0 && !mat_used[m]) {
+            mat_used[m] = 1;
+            work.push_back(m);
+        }
+    };
+    for (int32_t m : out.sphere_mat) use_mat(m);
+    for (int32_t m : out.msph_mat) use_mat(m);
+    for (int32_t m : out.planar_mat) use_mat(m);
+    for (const auto& md : out.media) use_mat(md.phase_mat);
+    while (!work.empty()) {
+        const int m = work.back();
+        work.pop_back();
+        use_mat(out.materials[m].inner);
+        use_mat(out.materials[m].inner2);
+    }
+    std::vector<int> twork;
+    auto use_tex = [&](int t) {
+        if (t >= 0 && !tex_used[t]) {
+            tex_used[t] = 1;
+            twork.push_back(t);
+        }
+    };
+    use_tex(background_tex);
+    for (size_t i = 0; i < out.materials.size(); ++i)
+        if (mat_used[i]) use_tex(out.materials[i].tex);
+    while (!twork.empty()) {
+        const int t = twork.back();
+        twork.pop_back();
+        if (out.textures[t].type == rtk::T_CHECKER) {
+            use_tex(out.textures[t].a);
+            use_tex(out.textures[t].b);
+        }
+    }
+    for (size_t i = 0; i < out.textures.size(); ++i)
+        if (tex_used[i] && (out.textures[i].type == rtk::T_IMAGE || out.textures[i].type == rtk::T_NOISE))
+            out.features |= rtk::F_TEXFULL;
+    for (size_t i = 0; i < out.materials.size(); ++i) {
+        if (!mat_used[i]) continue;
+        const rtk::DMaterial& m = out.materials[i];
         if (m.type == rtk::M_DIFFUSE_LIGHT || m.type == rtk::M_ISOTROPIC || m.type == rtk::M_TRANSPARENT ||
             m.type == rtk::M_MIX)
             out.features |= rtk::F_MATFULL;
+    }
+    for (size_t i = 0; i < out.materials.size(); ++i) {
+        if (!mat_used[i]) continue;
+        const rtk::DMaterial& m = out.materials[i];
+        if (m.type == rtk::M_MIX) {
+            for (int sub : {m.inner, m.inner2}) {
+                int st = out.materials[sub].type;
+                if (st == rtk::M_MIX || (st == rtk::M_DIFFUSE_LIGHT && out.materials[sub].inner >= 0))
+                    return set_error(RT_EUNSUPPORTED, "Mix of Mix / of DiffuseLight-with-material is not on the kernel path yet");
+            }
+        }
+        if (m.type == rtk::M_DIFFUSE_LIGHT && m.inner >= 0) {
+            int st = out.materials[m.inner].type;
+            if (st == rtk::M_MIX || st == rtk::M_DIFFUSE_LIGHT)
+                return set_error(RT_EUNSUPPORTED, "DiffuseLight wrapping Mix/DiffuseLight is not on the kernel path yet");
+        }
+    }
     if (out.list_children.empty()) out.list_children.push_back(rtk::REF_NONE);
     return RT_OK;
 }

@@ -70,6 +70,10 @@ struct Obj {
     // planar
     V3 anchor, u, v, w, normal;
     double D = 0, area = 0;
+    // OBJ triangle: RemappedMaterial (obj.rs:20-29)
+    bool remap = false;
+    V3 rn[3];
+    double tex_ori[2] = {0, 0}, tex_u[2] = {0, 0}, tex_v[2] = {0, 0};
     // list / bvh / transform / medium
     std::vector<int> children;
     int left = -1, right = -1, child = -1;
@@ -107,6 +111,8 @@ struct HostWorld {
     std::vector<rtk::DPlanar> planars;
     std::vector<double> planar_area;
     std::vector<int32_t> planar_mat;
+    std::vector<int32_t> planar_remap;
+    std::vector<rtk::DRemap> remaps;
     std::vector<uint32_t> list_children;
     std::vector<rtk::DXform> xforms;
     std::vector<rtk::DMedium> media;

@@ -16,6 +16,7 @@ script the test-only oracle to compare against.
 """
 import ctypes as C
 import math
+import os
 
 import numpy as np
 
@@ -171,6 +172,13 @@ class Scene:
 
     def ConstantMedium(self, boundary, density, tex):
         return Hittable(self, self._c(self.api.constant_medium_new(self.s, boundary.h, float(density), tex.h)), "medium")
+
+    def Wavefont(self, obj_path, vanilla_material=True):
+        """Wavefont::new (shapes/obj.rs:117-134); returns the Hittables of its
+        per-model BVHs.  The reference's Option<Wavefont> is None when the OBJ
+        cannot be opened: here that raises RtError(RT_EINVAL)."""
+        rc = self.api.wavefront_load(self.s, os.fsencode(obj_path), 1 if vanilla_material else 0)
+        return Hittables(self, self._c(rc), "list")
 
 
 class Camera:

@@ -5,6 +5,7 @@ implementation of the ABI) and returns (world, lights, camera).
   C1  random_spheres(scene, 400, 100)     book-1 final scene, reference CPU size
   C2  random_spheres(scene, 1920, 512)    the headline benchmark (484 traced spp)
   C3  cornell_smoke(scene, 800, 1024)     reference cornell_box + a smoke box
+  C4  obj_terrain(scene, path, 1920, 256) synthetic 1M-triangle OBJ (write_terrain_obj)
   C5  final_scene(scene, 3840, 4096, 40)  reference final_scene, aspect 16/9
 
 Scene-construction randomness (the reference calls Random:: while building,
@@ -166,3 +167,89 @@ def final_scene(scene, image_width=800, samples_per_pixel=5000, max_depth=40, as
     cam.vec_up = (0.0, 1.0, 0.0)
     cam.defocus_angle_in_degrees = 0.0
     return world, lights, cam
+
+
+# ---------------------------------------------------------------- C4: synthetic OBJ mesh
+TERRAIN_MTL = """# two vanilla materials (obj.rs:289-298): Pm 1 -> Metal(Kd, Pr)
+newmtl chrome
+Kd 0.8 0.85 0.9
+Pm 1.0
+Pr 0.15
+newmtl gold
+Kd 0.9 0.7 0.3
+Pm 1.0
+Pr 0.45
+"""
+
+
+def terrain_height(x, z):
+    """Displacement of the C4 terrain and its analytic gradient."""
+    import numpy as np
+
+    h = 0.35 * np.sin(1.3 * x) * np.cos(1.1 * z) + 0.12 * np.sin(3.7 * x + 1.3) * np.sin(2.9 * z) \
+        + 0.04 * np.cos(9.0 * x - 7.0 * z)
+    hx = 0.35 * 1.3 * np.cos(1.3 * x) * np.cos(1.1 * z) + 0.12 * 3.7 * np.cos(3.7 * x + 1.3) * np.sin(2.9 * z) \
+        - 0.04 * 9.0 * np.sin(9.0 * x - 7.0 * z)
+    hz = -0.35 * 1.1 * np.sin(1.3 * x) * np.sin(1.1 * z) + 0.12 * 2.9 * np.sin(3.7 * x + 1.3) * np.cos(2.9 * z) \
+        + 0.04 * 7.0 * np.sin(9.0 * x - 7.0 * z)
+    return h, hx, hz
+
+
+def write_terrain_obj(directory, cells=707, extent=4.0):
+    """Writes terrain.obj + terrain.mtl: a (cells x cells)-quad displaced grid
+    over [-extent, extent]^2 (2*cells^2 triangles; cells=707 -> 999 698), every
+    corner `v/vt/vn` with one shared index, analytic vertex normals, texture
+    coordinates (i/cells, j/cells).  Two objects (x < 0: `chrome`, x >= 0:
+    `gold`) so the loader's per-model BVHs and usemtl handling are exercised.
+    Deterministic: the same cells give the same bytes."""
+    import numpy as np
+
+    os.makedirs(directory, exist_ok=True)
+    n = cells + 1
+    g = np.linspace(-extent, extent, n)
+    X, Z = np.meshgrid(g, g, indexing="ij")  # [i, j] -> (x_i, z_j)
+    H, HX, HZ = terrain_height(X, Z)
+    N = np.stack([-HX, np.ones_like(HX), -HZ], axis=-1)
+    N /= np.linalg.norm(N, axis=-1, keepdims=True)
+    U, V = np.meshgrid(np.arange(n) / cells, np.arange(n) / cells, indexing="ij")
+    obj = os.path.join(directory, "terrain.obj")
+    with open(os.path.join(directory, "terrain.mtl"), "w") as f:
+        f.write(TERRAIN_MTL)
+    with open(obj, "w") as f:
+        f.write("# synthetic C4 terrain: %d x %d cells, %d triangles\nmtllib terrain.mtl\n" % (cells, cells, 2 * cells * cells))
+        np.savetxt(f, np.stack([X.ravel(), H.ravel(), Z.ravel()], 1), fmt="v %.6f %.6f %.6f")
+        np.savetxt(f, np.stack([U.ravel(), V.ravel()], 1), fmt="vt %.6f %.6f")
+        np.savetxt(f, N.reshape(-1, 3), fmt="vn %.6f %.6f %.6f")
+        idx = np.arange(n * n).reshape(n, n) + 1  # 1-based
+        a, b, c, d = idx[:-1, :-1], idx[1:, :-1], idx[1:, 1:], idx[:-1, 1:]
+        half = cells // 2
+        for name, sl in (("chrome", slice(0, half)), ("gold", slice(half, cells))):
+            f.write("o terrain_%s\nusemtl %s\n" % (name, name))
+            # two counter-clockwise (seen from +y) triangles per cell
+            t1 = np.stack([a[sl], d[sl], c[sl]], -1).reshape(-1, 3)
+            t2 = np.stack([a[sl], c[sl], b[sl]], -1).reshape(-1, 3)
+            tris = np.stack([t1, t2], 1).reshape(-1, 3)
+            np.savetxt(f, np.repeat(tris, 3, axis=1), fmt="f %d/%d/%d %d/%d/%d %d/%d/%d")
+    return obj
+
+
+def obj_terrain(scene, obj_path, image_width=1920, samples_per_pixel=256, max_depth=50):
+    """C4: world = Hittables{ Wavefont(terrain.obj) (one BVH per
+    model), a glass and a diffuse sphere }, sky background."""
+    world = scene.Hittables()
+    world.add(scene.Wavefont(obj_path, True))
+    world.add(scene.Sphere((-0.9, 1.0, 0.6), 0.45, scene.Dielectric(scene.SolidColor((1.0, 1.0, 1.0)), 1.5)))
+    world.add(scene.Sphere((1.1, 0.95, -0.3), 0.4, scene.Lambertian(scene.SolidColor((0.7, 0.2, 0.15)))))
+    cam = Camera()
+    cam.aspect_ratio = 16.0 / 9.0
+    cam.image_width = image_width
+    cam.samples_per_pixel = samples_per_pixel
+    cam.max_depth = max_depth
+    cam.vertical_fov_in_degrees = 40.0
+    cam.look_from = (0.0, 3.4, 6.8)
+    cam.look_at = (0.0, 0.0, 0.0)
+    cam.vec_up = (0.0, 1.0, 0.0)
+    cam.defocus_angle_in_degrees = 0.0
+    cam.focus_distance = 10.0
+    cam.background = scene.SkyGradient((1.0, 1.0, 1.0), (0.5, 0.7, 1.0))
+    return world, None, cam

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Algorithmic work per traced sample for the C2 workload.
+"""Algorithmic work per traced sample for the C2 / C4 workloads.
+
+  python scripts/work_counts.py [c2|c4]
 
 Runs the TEST-ONLY oracle (reference algorithm, reference BVH topology,
 recursive ray_color) instrumented on a C2 subsample -- every 8th row of the
@@ -33,6 +35,7 @@ WEIGHTS = {
     "sphere_records": 21 + 6,  # record + uv (the reference computes uv for every record)
     "quad_tests": 49,
     "tri_tests": 49,
+    "planar_records": 20 + 25,  # HitRecord::new + RemappedMaterial::remap_record (C4 meshes)
     "lambert": 70,
     "metal": 46,
     "dielectric": 50,
@@ -43,13 +46,22 @@ WEIGHTS = {
 BYTES = {"bvh_node_tests": 64, "sphere_tests": 36, "quad_tests": 132, "tri_tests": 132}
 
 
-def main(row_stride=8, spp=16, threads=0):
+def main(workload="c2", row_stride=None, spp=None, threads=0):
     capi = importlib.import_module("raytracer-2025_amd.capi")
     rt = importlib.import_module("raytracer-2025_amd.raytracer")
     scenes = importlib.import_module("raytracer-2025_amd.scenes")
     api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "liboracle.so")), "orc_", capi.ORACLE_EXTRAS)
     scene = rt.Scene(api)
-    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    if workload == "c2":
+        row_stride, spp = row_stride or 8, spp or 16
+        world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+        desc = "C2 book-1 random spheres 1920x1080, max_depth 50 (per traced sample)"
+    else:
+        import tempfile
+        row_stride, spp = row_stride or 16, spp or 4
+        obj = scenes.write_terrain_obj(os.path.join(tempfile.gettempdir(), "rt_terrain_707"), 707)
+        world, lights, cam = scenes.obj_terrain(scene, obj, 1920, spp)
+        desc = "C4 synthetic 1M-triangle OBJ terrain 1920x1080, max_depth 50 (per traced sample)"
     c = cam.to_c()
     opts = capi.RtRenderOpts()
     api.render_opts_default(ctypes.byref(opts))
@@ -67,17 +79,17 @@ def main(row_stride=8, spp=16, threads=0):
     flops = sum(per[k] * w for k, w in WEIGHTS.items())
     bytes_ = sum(per[k] * w for k, w in BYTES.items())
     out = {
-        "workload": "C2 book-1 random spheres 1920x1080, max_depth 50 (per traced sample)",
+        "workload": desc,
         "sample": f"every {row_stride}th row, {spp} spp ({cam.sqrt_spp}^2 strata), seed 1, oracle (reference topology)",
         "samples": samples,
         "per_sample": per,
         "weights_flops": WEIGHTS,
         "flops_per_sample": flops,
         "cache_bytes_per_sample": bytes_,
-        "hbm_bytes_per_pixel": 24 * 22 + 12,
+        "hbm_bytes_per_pixel": 24 * cam.sqrt_spp + 12,
         "cpu_seconds": st.render_ms / 1e3,
     }
-    path = os.path.join(ROOT, "bench_data", "work_counts_c2.json")
+    path = os.path.join(ROOT, "bench_data", "work_counts_%s.json" % workload)
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
@@ -85,4 +97,4 @@ def main(row_stride=8, spp=16, threads=0):
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "c2")

@@ -165,7 +165,8 @@ def test_sah_matches_reference_topology(gpu, rt, scenes, which):
     assert np.all(rmse < 1e-6)
 
 
-@pytest.mark.parametrize("name", ["c1_64x36_s16_seed7", "c3_48x48_s16_seed7", "c5_64x36_s16_seed7"])
+@pytest.mark.parametrize("name", ["c1_64x36_s16_seed7", "c3_48x48_s16_seed7", "c4_64x36_s16_seed7",
+                                  "c5_64x36_s16_seed7"])
 def test_gpu_vs_golden_fixture(gpu, rt, name):
     """GPU against the committed oracle frames (tests/golden/), no oracle at run time."""
     import importlib
@@ -181,4 +182,121 @@ def test_gpu_vs_golden_fixture(gpu, rt, name):
     ref = np.load(os.path.join(ROOT, "tests", "golden", name + ".npy"))
     rmse = rmse_per_channel(lin, ref)
     print(name, "RMSE vs golden", rmse)
+    assert np.all(rmse < TOL)
+
+
+# ---------------------------------------------------------------- C4: OBJ meshes (mesh tier)
+@pytest.fixture(scope="module")
+def terrain24(scenes, tmp_path_factory):
+    return scenes.write_terrain_obj(str(tmp_path_factory.mktemp("terrain24")), 24)
+
+
+def test_c4_obj_terrain_small(gpu, oracle, rt, scenes, capi, terrain24):
+    """Triangles in per-model BVHs under RemappedMaterial (obj.rs:20-81), Metal
+    from MTL Pm 1, plus a glass and a diffuse sphere: the mesh kernel tier."""
+    out, st = render_both(gpu, oracle, rt, lambda s: scenes.obj_terrain(s, terrain24, 96, 16))
+    check(out)
+    assert st["gpu"].panics == 0 and st["oracle"].panics == 0
+    scene = rt.Scene(gpu)
+    world, _, cam = scenes.obj_terrain(scene, terrain24, 8, 1)
+    import ctypes
+    info = capi.RtWorldInfo()
+    gpu.check(gpu.world_info_get(scene.s, world.h, -1, cam.background.h, 0, ctypes.byref(info)))
+    assert info.kernel_tier == 1
+
+
+def test_c4_sah_matches_reference_topology(gpu, rt, scenes, terrain24):
+    scene = rt.Scene(gpu)
+    world, lights, cam = scenes.obj_terrain(scene, terrain24, 96, 9)
+    a, _, _ = cam.render(world, lights, seed=5, flags=0)
+    b, _, _ = cam.render(world, lights, seed=5, flags=1)
+    assert np.all(rmse_per_channel(a, b) < 1e-6)
+
+
+OBJ_MTL = """newmtl lamp
+Kd 0.6 0.6 0.6
+Pm 1
+Pr 0.3
+Ke 3 2 1
+newmtl ghost
+Kd 0.7 0.5 0.5
+Pm 1
+Pr 0.1
+d 0.4
+newmtl glass
+Kd 1 1 1
+Tf 1 1 1
+Ni 1.5
+"""
+OBJ_BENT = """mtllib m.mtl
+v -1 0 -1
+v 1 0 -1
+v 1 0 1
+v -1 0 1
+v 0 1 0
+vt 0 0
+vt 1 0
+vt 1 1
+vt 0 1
+vn 0.4 1 0
+vn -0.2 1 0.3
+vn 0 1 -0.5
+vn 0.1 0.2 1
+o floor
+usemtl ghost
+f 1/1/1 4/4/2 3/3/3 2/2/4
+o tent
+usemtl glass
+f 1/1/2 2/2/3 5/3/1
+f 3/3/4 4/4/1 5/1/2
+o lamp
+usemtl lamp
+f 2/2/1 3/3/2 5/4/3
+"""
+
+
+def test_c4_obj_full_tier_materials(gpu, oracle, rt, tmp_path):
+    """Ke -> DiffuseLight(Metal), d -> Mix(Transparent, Metal), Tf -> Dielectric,
+    bent vertex normals: an OBJ that needs the full kernel tier."""
+    (tmp_path / "m.mtl").write_text(OBJ_MTL)
+    (tmp_path / "bent.obj").write_text(OBJ_BENT)
+
+    def build(s):
+        world = s.Hittables()
+        world.add(s.Wavefont(str(tmp_path / "bent.obj")))
+        world.add(s.Sphere((0, -100.5, 0), 100, s.Lambertian(s.SolidColor((0.4, 0.5, 0.4)))))
+        cam = rt.Camera()
+        cam.aspect_ratio = 1.0
+        cam.image_width = 64
+        cam.samples_per_pixel = 16
+        cam.max_depth = 12
+        cam.vertical_fov_in_degrees = 60.0
+        cam.look_from = (0.4, 1.8, 2.6)
+        cam.look_at = (0.0, 0.2, 0.0)
+        cam.background = s.SkyGradient((1.0, 1.0, 1.0), (0.5, 0.7, 1.0))
+        return world, None, cam
+
+    out, st = render_both(gpu, oracle, rt, build)
+    check(out, min_exact=0.8)
+    assert st["gpu"].panics == st["oracle"].panics
+
+
+def test_c4_full_size_mesh_rows(gpu, oracle, rt, scenes, tmp_path):
+    """BASELINE configs[3] geometry: the 1M-triangle terrain at 1920x1080.  Two
+    shard rows (0 and 540) at 4 spp against the oracle on the same 1M-triangle
+    world, and the whole frame at 1 spp for finiteness / no panics."""
+    p = scenes.write_terrain_obj(str(tmp_path), 707)
+    out = {}
+    for name, api in (("gpu", gpu), ("oracle", oracle)):
+        scene = rt.Scene(api)
+        world, lights, cam = scenes.obj_terrain(scene, p, 1920, 4)
+        lin, _, st = cam.render(world, lights, seed=11, row_offset=0, row_stride=540)
+        assert lin.shape == (2, 1920, 3) and st.panics == 0
+        out[name] = lin
+        if name == "gpu":
+            cam.samples_per_pixel = 1
+            full, _, st1 = cam.render(world, lights, seed=11)
+            assert full.shape == (1080, 1920, 3) and np.isfinite(full).all() and st1.panics == 0
+    rmse = rmse_per_channel(out["gpu"], out["oracle"])
+    print("C4 full-size rows RMSE", rmse)
     assert np.all(rmse < TOL)
