@@ -117,7 +117,7 @@ def main():
     ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) on GPU nodes; gloo only to rehearse ranks on one GPU")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-row-stride", type=int, default=2)
-    ap.add_argument("--cpu-spp", type=int, default=16)
+    ap.add_argument("--cpu-spp", type=int, default=None, help="default: 64 (c2), 36 (c4) -> ~10 s of oracle work")
     args = ap.parse_args()
     if args.spp is None:
         args.spp = 512 if args.workload == "c2" else 256
@@ -257,8 +257,8 @@ def main():
             },
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride if args.workload == "c2" else 8,
-                                                args.cpu_spp if args.workload == "c2" else 4, args.workload)
+            cpu_spp = args.cpu_spp or (64 if args.workload == "c2" else 36)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, cpu_spp, args.workload)
         print(json.dumps(line), flush=True)
     if distributed:
         dist.barrier()

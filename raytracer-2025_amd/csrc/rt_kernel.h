@@ -9,7 +9,8 @@
 #define RT_BLOCK 256        // 4 waves of 64
 // traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
 #define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
-#define RT_STACK_MESH 32    // 64 KiB: 2 blocks per CU (deep triangle BVHs; VGPR-bound at 2 anyway)
+#define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column (mesh tier)
+#define RT_STACK_MESH_MAX 64
 #define RT_STACK_FULL 32    // 64 KiB: 2 blocks per CU
 
 namespace rtk {
@@ -38,7 +39,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" uint32_t rtk_stack_entries(int tier);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int tier, int grid, void* params_dev);
+                                       int tier, int grid, void* params_dev, void* stack_ovf);
 // device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);

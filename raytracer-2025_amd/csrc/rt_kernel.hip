@@ -280,12 +280,29 @@ struct HitInfo {
 // The per-lane traversal stack: entry k of lane l at stk[k * RT_BLOCK] (the
 // pointer is already offset by the lane), {ref, entry distance as f32 rounded
 // down} -- one ds_write_b64 / ds_read_b64 per push / pop, 64 distinct banks
-// per half-wave.
-struct Stack {
+// per half-wave.  With OVF, entries k >= CAP (deep triangle BVHs) live in the
+// lane's column of a global overflow buffer, [k - CAP][lane of the grid], so
+// the LDS part stays small enough for 4 blocks per CU.
+template <uint32_t CAP, bool OVF>
+struct StackT {
     uint2* base;
-    __device__ __forceinline__ void push(uint32_t sp, uint32_t ref, float t) { base[sp * RT_BLOCK] = make_uint2(ref, __float_as_uint(t)); }
-    __device__ __forceinline__ uint2 at(uint32_t sp) const { return base[sp * RT_BLOCK]; }
+    RT_GLOBAL uint2* ovf;
+    uint32_t stride;
+    __device__ __forceinline__ void push(uint32_t sp, uint32_t ref, float t) {
+        const uint2 v = make_uint2(ref, __float_as_uint(t));
+        if (OVF && sp >= CAP)
+            ovf[(sp - CAP) * stride] = v;
+        else
+            base[sp * RT_BLOCK] = v;
+    }
+    __device__ __forceinline__ uint2 at(uint32_t sp) const {
+        if (OVF && sp >= CAP) return ovf[(sp - CAP) * stride];
+        return base[sp * RT_BLOCK];
+    }
 };
+template <int TIER>
+using StackFor = StackT<TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
+                        TIER == TIER_MESH>;
 __device__ __forceinline__ float f32_down(double x) {
     float f = (float)x;  // round-to-nearest; step one ulp down when it rounded up
     if ((double)f > x) {
@@ -309,7 +326,7 @@ struct Closest {
 // here from the data in its slot (sphere.rs:77-108); other children get the
 // f32 slab test, and the hit ones are walked near-first with the farther one
 // pushed with its entry distance.
-template <class OnHit>
+template <class Stack, class OnHit>
 __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
                                                double a, double tmin, float tmin_f, Closest& cl, Stack& stk,
                                                uint32_t& sp, OnHit&& on_hit) {
@@ -351,6 +368,7 @@ __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx,
 }
 
 // Pops until an entry whose box can still hold a hit closer than c.
+template <class Stack>
 __device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t sp0, float c_f) {
     while (sp > sp0) {
         --sp;
@@ -364,6 +382,7 @@ constexpr float NO_CULL = -__builtin_huge_valf();
 
 // Closest t of a medium boundary (no media inside, no records) -- the two
 // boundary.hit calls of volume.rs:44-48.
+template <class Stack>
 __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax, Stack& stk,
                            uint32_t sp0, double& tbest) {
     Ray r = r0;
@@ -450,7 +469,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
 // and keeps the first minimum: the same closest hit up to exact t ties).
 template <int TIER>
-__device__ bool trace(const SceneView& S, const Ray& wr, Stack& stk, const Rng& rng, HitInfo& hit, Diag& dg) {
+__device__ bool trace(const SceneView& S, const Ray& wr, StackFor<TIER>& stk, const Rng& rng, HitInfo& hit, Diag& dg) {
     constexpr bool FULL = TIER == TIER_FULL;
     RT_DIAG_ONLY(unsigned long long it = 0;)
     const double tmin = 1e-8;
@@ -757,7 +776,7 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
 template <int TIER>
-__device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, Stack& stk,
+__device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, StackFor<TIER>& stk,
                                        bool& panic, Diag& dg) {
     constexpr bool FULL = TIER == TIER_FULL;
     uint32_t ovf = 0;
@@ -930,7 +949,7 @@ __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D
 #define RT_BASIC_WAVES 4  // waves per SIMD the basic tier is register-allocated for
 #endif
 #ifndef RT_MESH_WAVES
-#define RT_MESH_WAVES 2
+#define RT_MESH_WAVES 4  // 4-wave budget (some spills) beats 2 waves: 164.7 vs 263.8 ms (C4, 64 spp)
 #endif
 
 // Launch parameters live in device memory and are read where they are used
@@ -941,6 +960,7 @@ struct KParams {
     uint32_t* queue;
     double* partial;
     unsigned long long* stats;
+    RT_GLOBAL uint2* stack_ovf;  // mesh tier: [stack_need - RT_STACK_MESH][grid * RT_BLOCK] entries
 };
 
 template <int TIER>
@@ -952,7 +972,8 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIE
     uint32_t* queue = P->queue;
     constexpr int STACK = TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
     __shared__ uint2 stack_lds[STACK * RT_BLOCK];
-    Stack stk{stack_lds + threadIdx.x};
+    StackFor<TIER> stk{stack_lds + threadIdx.x,
+                       P->stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x, gridDim.x * RT_BLOCK};
     const uint32_t lane = __lane_id();
 
     Rng rng;
@@ -1091,18 +1112,18 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
 // ------------------------------------------------------------------ host launchers
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL;
-    if ((features & full) || stack_need > RT_STACK_MESH) return rtk::TIER_FULL;
+    if ((features & full) || stack_need > RT_STACK_MESH_MAX) return rtk::TIER_FULL;
     if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;
 }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
-    return tier == rtk::TIER_FULL ? RT_STACK_FULL : (tier == rtk::TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
+    return tier == rtk::TIER_FULL ? RT_STACK_FULL : (tier == rtk::TIER_MESH ? RT_STACK_MESH_MAX : RT_STACK_BASIC);
 }
 
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int tier, int grid, void* params_dev) {
+                                       int tier, int grid, void* params_dev, void* stack_ovf) {
     rtk::KParams K;
     K.S = *view;
     rtk::Frame& F = K.F;
@@ -1127,6 +1148,7 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     K.queue = queue;
     K.partial = partial;
     K.stats = stats;
+    K.stack_ovf = (RT_GLOBAL uint2*)stack_ovf;
     rtk::KParams* Pd = (rtk::KParams*)params_dev;
     hipError_t e = hipMemcpyAsync(Pd, &K, sizeof K, hipMemcpyHostToDevice, stream);
     if (e != hipSuccess) return e;

@@ -27,6 +27,8 @@ struct DeviceWorld {
     size_t partial_bytes = 0;
     float* out = nullptr;
     size_t out_bytes = 0;
+    void* stack_ovf = nullptr;  // mesh tier: traversal-stack entries beyond the LDS part
+    size_t stack_ovf_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     // last async render
     bool pending = false;
@@ -48,6 +50,7 @@ void destroy_device_world(DeviceWorld* d) {
     if (d->params) (void)hipFree(d->params);
     if (d->partial) (void)hipFree(d->partial);
     if (d->out) (void)hipFree(d->out);
+    if (d->stack_ovf) (void)hipFree(d->stack_ovf);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
     delete d;
@@ -111,6 +114,16 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
                                         std::to_string(stack_cap));
+    if (tier == rtk::TIER_MESH && hw.stack_need > RT_STACK_MESH) {
+        const size_t need = (size_t)(hw.stack_need - RT_STACK_MESH) * d->grid[tier] * RT_BLOCK * sizeof(uint64_t);
+        if (need > d->stack_ovf_bytes) {
+            if (d->stack_ovf) (void)hipFree(d->stack_ovf);
+            d->stack_ovf = nullptr;
+            d->stack_ovf_bytes = 0;
+            if ((e = hipMalloc(&d->stack_ovf, need)) != hipSuccess) return hip_fail(e, "hipMalloc stack overflow");
+            d->stack_ovf_bytes = need;
+        }
+    }
     std::vector<char> blob;
     size_t o_nodes = put(blob, hw.nodes), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
            o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
@@ -274,7 +287,8 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     float* out = dev_out ? dev_out : d->out;
     const bool run = f.rows > 0 && f.max_depth > 0;
     if (run) {
-        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->tier, d->grid[d->tier], d->params);
+        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->tier, d->grid[d->tier], d->params,
+                             d->stack_ovf);
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
     } else if (f.rows > 0) {
         // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)

@@ -2,7 +2,8 @@
 """Interleaved A/B of kernel variants (raytracer-2025_amd/librt_ab_*.so, built
 by `make -C raytracer-2025_amd ab`) in one process on the C2 scene: each
 variant renders the same frame; path-kernel time from the library's HIP
-events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]"""
+events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]
+AB_WORKLOAD=c4 renders the C4 1M-triangle terrain instead of C2."""
 import ctypes
 import glob
 import importlib
@@ -27,7 +28,14 @@ runs = {}
 for n in names:
     api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", f"librt_ab_{n}.so")), "rt_")
     scene = rt.Scene(api)
-    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    if os.environ.get("AB_WORKLOAD", "c2") == "c4":
+        import tempfile
+        obj = os.path.join(tempfile.gettempdir(), "rt_terrain_707", "terrain.obj")
+        if not os.path.exists(obj):
+            scenes.write_terrain_obj(os.path.dirname(obj), 707)
+        world, lights, cam = scenes.obj_terrain(scene, obj, 1920, spp)
+    else:
+        world, lights, cam = scenes.random_spheres(scene, 1920, spp)
     lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)  # warm-up
     runs[n] = (scene, world, lights, cam, lin)
 res = {n: [] for n in names}

@@ -1,7 +1,16 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 output (gpurun_out/prof*) into profiles/<round>/:
-kernel_stats.csv (copied), pmc_summary.json (per-launch averages of every
-counter for rt_path_kernel) and pmc_c2.json (HBM bytes per launch for bench.py)."""
+"""Summarise one scripts/bench_box.sh run (gpurun_out/box/) into
+profiles/<round>/:
+
+  kernel_stats_<w>.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  pmc_<w>.json           HBM bytes per launch of rt_path_kernel, for bench.py
+  pmc_summary.json       per-launch counters of every workload + derived values
+  bench_<w>.json         the bench line of that run
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE (KiB) come
+from separate --pmc passes; FETCH_SIZE is doubled (gfx950 tallies 128-B read
+requests at 64 B), WRITE_SIZE is taken as is.
+  python scripts/summarize_profiles.py [round] [src]"""
 import collections
 import csv
 import glob
@@ -23,33 +32,48 @@ def per_launch(path, kernel="rt_path_kernel"):
     return {c: v / len(disp[c]) for c, v in agg.items()}
 
 
-def main(rnd="r01", srcs=("gpurun_out/prof", "gpurun_out/prof2")):
+def kernel_avg_ns(stats_csv, kernel="rt_path_kernel"):
+    for r in csv.DictReader(open(stats_csv)):
+        if kernel in r["Name"]:
+            return float(r["AverageNs"]), r["Name"], int(r["Calls"])
+    return None, None, 0
+
+
+def main(rnd="r01", src="gpurun_out/box"):
+    src = os.path.join(ROOT, src)
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    counters = {}
-    for src in srcs:
-        for f in sorted(glob.glob(os.path.join(ROOT, src, "*", "run_counter_collection.csv"))):
-            counters.update(per_launch(f))
-        ks = os.path.join(ROOT, src, "trace", "run_kernel_stats.csv")
+    summary = {}
+    for w in ("c2", "c4"):
+        entry = {}
+        ks = os.path.join(src, "trace_" + w, "run_kernel_stats.csv")
         if os.path.exists(ks):
-            shutil.copy(ks, os.path.join(dst, "kernel_stats_c2.csv"))
-    out = {"kernel": "rt_path_kernel<false> (C2, 1920x1080x484 spp)", "per_launch": counters}
-    c = counters
-    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
-        out["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"])
-    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        # rocprofv3 FETCH_SIZE / WRITE_SIZE are KiB; see MI355X_MICROARCH.md §HBM
-        out["hbm_bytes_per_launch"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
-        out["hbm_note"] = ("FETCH_SIZE + WRITE_SIZE (KiB -> B), uncorrected: the ×2 gfx950 FETCH correction is for "
-                           "16-B/lane streaming reads; the path kernel's reads are L2/MALL-resident scene gathers")
-    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
-        out["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-    if "hbm_bytes_per_launch" in out:
-        json.dump({"hbm_bytes_per_launch": out["hbm_bytes_per_launch"], "source": "profiles/%s/pmc_summary.json" % rnd},
-                  open(os.path.join(dst, "pmc_c2.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1))
+            shutil.copy(ks, os.path.join(dst, "kernel_stats_%s.csv" % w))
+            ns, name, calls = kernel_avg_ns(ks)
+            entry.update({"kernel": name, "calls": calls, "avg_ms": ns / 1e6 if ns else None})
+        counters = {}
+        for f in sorted(glob.glob(os.path.join(src, "*_" + w, "run_counter_collection.csv"))):
+            counters.update(per_launch(f))
+        entry["per_launch"] = counters
+        if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
+            fetch = 2.0 * counters["FETCH_SIZE"] * 1024.0
+            write = counters["WRITE_SIZE"] * 1024.0
+            entry["hbm_read_bytes_per_launch"] = fetch
+            entry["hbm_write_bytes_per_launch"] = write
+            entry["hbm_bytes_per_launch"] = fetch + write
+            json.dump({"hbm_bytes_per_launch": fetch + write, "read": fetch, "write": write,
+                       "method": "2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), separate --pmc passes, MI355X_MICROARCH.md §HBM",
+                       "source": "profiles/%s/pmc_summary.json" % rnd},
+                      open(os.path.join(dst, "pmc_%s.json" % w), "w"), indent=1)
+        bl = os.path.join(src, "bench_%s.log" % w)
+        if os.path.exists(bl):
+            lines = [l for l in open(bl) if l.startswith("{")]
+            if lines:
+                open(os.path.join(dst, "bench_%s.json" % w), "w").write(lines[-1])
+        summary[w] = entry
+    json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(summary, indent=1))
 
 
 if __name__ == "__main__":
-    main(*(sys.argv[1:2] or []))
+    main(*sys.argv[1:])
