@@ -204,6 +204,21 @@ int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_ca
 /* Waits for the last rt_render_device on this scene and reports its stats. */
 int32_t rt_render_device_wait(rt_scene* s, rt_stats* stats);
 
+/* ---- Output stage ---------------------------------------------------------- */
+/* Color::to_rgb (utils/color.rs:27-36) of a device-resident linear framebuffer
+ * (n_values f32 -> u8, toon_map 0 = None, 1 = ACES), enqueued on `stream`.
+ * rt_render's out_srgb is the same conversion made from the f64 pixel sums. */
+int32_t rt_to_rgb_device(const float* linear_device, uint8_t* srgb_device, uint64_t n_values, int32_t toon_map,
+                         void* stream);
+/* img.save(path) with std::fs::create_dir_all of its parent (main.rs:39-47):
+ * 8-bit RGB PNG, row-major, y down. */
+int32_t rt_write_png(const char* path, uint32_t width, uint32_t height, const uint8_t* rgb);
+/* Camera::from_json (camera.rs:119-159) with the path given directly (the
+ * reference looks in RTW_IMAGES, then ./assets): the CameraParams fields
+ * (camera.rs:33-43) over rt_camera_default; a missing field or a malformed
+ * file is RT_EINVAL (the reference's Err). */
+int32_t rt_camera_from_json(const char* path, rt_camera* cam);
+
 #ifdef __cplusplus
 }
 #endif

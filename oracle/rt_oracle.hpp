@@ -624,11 +624,20 @@ struct Mix : Material {  // material.rs:220-268 (constant ratio form, Mix::new)
 struct RemappedMaterial : Material {
     std::shared_ptr<Material> material;
     Vec3 tex_ori, tex_u, tex_v;  // z = 0 (get_two_values, obj.rs:112-115)
+    std::optional<Vec3> u_vec, v_vec;
     Vec3 normal[3];
+    std::shared_ptr<Texture> normal_tex;  // None = null
     HitRecord remap_record(const HitRecord& rec) const {
         Vec3 tex_coord = tex_ori + rec.u * tex_u + rec.v * tex_v;
         Vec3 n = expect_unit((1.0 - rec.u - rec.v) * normal[0] + rec.u * normal[1] + rec.v * normal[2],
                              "called `Option::unwrap()` on a `None` value (obj.rs:40)");
+        if (normal_tex) {
+            Vec3 normal_color = normal_tex->value(tex_coord.e[0], tex_coord.e[1], rec.p);
+            normal_color = normal_color * 2.0 - Vec3(1.0, 1.0, 1.0);
+            if (!u_vec || !v_vec) throw Panic("called `Option::unwrap()` on a `None` value (obj.rs:47)");
+            Vec3 normal_raw = *u_vec * normal_color.e[0] + *v_vec * normal_color.e[1] + n * normal_color.e[2];
+            n = expect_unit(normal_raw, "The mapped normal can't normalized!");
+        }
         HitRecord h = rec;
         h.normal = n;
         h.u = tex_coord.e[0];

@@ -246,6 +246,7 @@ int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
     };
     auto transparent = std::make_shared<Transparent>();
     std::vector<std::shared_ptr<Material>> mats;
+    std::vector<std::shared_ptr<Texture>> normals;
     for (const ObjMaterial& m : f.materials) {
         std::shared_ptr<Texture> base;
         if (!m.diffuse_texture.empty()) {
@@ -257,7 +258,6 @@ int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
         } else {
             throw Panic("The material should at least have one diffuse!");
         }
-        if (!m.normal_texture.empty()) return fail(RT_EUNSUPPORTED, "normal maps are not supported");
         const double roughness = param(m, "Pr", 0.5), metallic = param(m, "Pm", 0.0);
         const double ior = m.has_optical_density ? m.optical_density : 1.45;
         double spec_trans = 0.0;
@@ -284,6 +284,19 @@ int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
         if (!m.dissolve_texture.empty()) return fail(RT_EUNSUPPORTED, "map_d is not supported");
         if (m.has_dissolve && m.dissolve < 1.0) mat = std::make_shared<Mix>(transparent, mat, m.dissolve);
         mats.push_back(mat);
+        std::shared_ptr<Texture> ntex;  // obj.rs:324-343
+        if (!m.normal_texture.empty()) {
+            std::string fname = m.normal_texture;
+            if (fname.rfind("-bm", 0) == 0) {
+                std::istringstream is(fname.substr(3));
+                std::string w, last;
+                while (is >> w) last = w;
+                if (!last.empty()) fname = last;
+            }
+            if (exists(prefix + "/" + fname)) return fail(RT_EUNSUPPORTED, "normal-map images are not supported");
+            ntex = std::make_shared<ImageTexture>();  // missing: cyan
+        }
+        normals.push_back(ntex);
     }
     auto objs = std::make_unique<Hittables>();
     auto empty = std::make_shared<EmptyMaterial>();
@@ -311,6 +324,16 @@ int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
             rm->normal[0] = three(o.normals, i0);
             rm->normal[1] = three(o.normals, i1);
             rm->normal[2] = three(o.normals, i2);
+            rm->normal_tex = normals[mi];
+            {  // uv_local_to_world (obj.rs:196-210)
+                const Vec3 tu = rm->tex_u, tv = rm->tex_v, wu = p2 - p1, wv = p3 - p1;
+                const double ua = tv.e[1] / (-tu.e[1] * tv.e[0] + tu.e[0] * tv.e[1]);
+                const double ub = tu.e[1] / (tu.e[1] * tv.e[0] - tu.e[0] * tv.e[1]);
+                const double va = tv.e[0] / (tu.e[1] * tv.e[0] - tu.e[0] * tv.e[1]);
+                const double vb = tu.e[0] / (-tu.e[1] * tv.e[0] + tu.e[0] * tv.e[1]);
+                rm->u_vec = from_vec3(wu * ua + wv * ub);
+                rm->v_vec = from_vec3(wu * va + wv * vb);
+            }
             auto tri = make_triangle(p1, p2 - p1, p3 - p1, rm);
             if (tri) v.push_back(std::move(tri));
         }

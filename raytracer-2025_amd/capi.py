@@ -113,6 +113,9 @@ SIGNATURES = {
     "shard_rows": (_U, [C.POINTER(RtCamera), C.POINTER(RtRenderOpts)]),
     "render_device": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _P]),
     "render_device_wait": (_I, [_P, C.POINTER(RtStats)]),
+    "to_rgb_device": (_I, [_P, _P, C.c_uint64, _I, _P]),
+    "write_png": (_I, [C.c_char_p, C.c_uint32, C.c_uint32, _P]),
+    "camera_from_json": (_I, [C.c_char_p, C.POINTER(RtCamera)]),
     "world_info_get": (_I, [_P, _I, _I, _I, _U, C.POINTER(RtWorldInfo)]),
 }
 

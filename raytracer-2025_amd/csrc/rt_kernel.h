@@ -9,9 +9,9 @@
 #define RT_BLOCK 256        // 4 waves of 64
 // traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
 #define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
-#define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column (mesh tier)
-#define RT_STACK_MESH_MAX 64
-#define RT_STACK_FULL 32    // 64 KiB: 2 blocks per CU
+#define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
+#define RT_STACK_FULL 16    // (mesh and full tiers)
+#define RT_STACK_MAX 64     // LDS + overflow entries (mesh and full tiers)
 
 namespace rtk {
 // Kernel tiers: the launcher picks the smallest that covers the flattened world.
@@ -38,8 +38,10 @@ struct rtk_frame_desc {
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" uint32_t rtk_stack_entries(int tier);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
-                                       double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int tier, int grid, void* params_dev, void* stack_ovf);
+                                       double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
+                                       int toon, hipStream_t stream, int tier, int grid, void* params_dev,
+                                       void* stack_ovf);
+extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream);
 // device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);

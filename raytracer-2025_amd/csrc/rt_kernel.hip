@@ -269,12 +269,25 @@ __device__ __forceinline__ Ray xf_ray(const DXform& X, const Ray& r) {
 }
 
 constexpr int MAX_XF = 2;
+// The Transforms entered on the way to a hit, innermost last.  Two named
+// fields, not an array: a dynamically indexed private array is placed in
+// scratch memory by the compiler.
+struct XfIds {
+    uint32_t a = 0, b = 0;
+    __device__ __forceinline__ uint32_t get(uint32_t k) const { return k == 0 ? a : b; }
+    __device__ __forceinline__ void set(uint32_t k, uint32_t v) {
+        if (k == 0)
+            a = v;
+        else
+            b = v;
+    }
+};
 
 struct HitInfo {
     double t;
     uint32_t ref;
     uint32_t nxf;
-    uint32_t xf[MAX_XF];
+    XfIds xf;
 };
 
 // The per-lane traversal stack: entry k of lane l at stk[k * RT_BLOCK] (the
@@ -302,7 +315,7 @@ struct StackT {
 };
 template <int TIER>
 using StackFor = StackT<TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
-                        TIER == TIER_MESH>;
+                        TIER != TIER_BASIC>;
 __device__ __forceinline__ float f32_down(double x) {
     float f = (float)x;  // round-to-nearest; step one ulp down when it rounded up
     if ((double)f > x) {
@@ -388,7 +401,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
     Ray r = r0;
     RayF rf = make_rayf(r);
     double a = len2(r.d);
-    uint32_t xfs[MAX_XF];
+    XfIds xfs;
     uint32_t nxf = 0;
     uint32_t sp = sp0;
     uint32_t cur = root;
@@ -442,7 +455,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             case K_XFORM: {
                 const DXform& X = S.xforms[idx];
                 stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
-                xfs[nxf++] = idx;
+                xfs.set(nxf++, idx);
                 r = xf_ray(X, r);
                 rf = make_rayf(r);
                 a = len2(r.d);
@@ -452,7 +465,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             case K_POPXF: {
                 --nxf;
                 r = r0;
-                for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
+                for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs.get(k)], r);
                 rf = make_rayf(r);
                 a = len2(r.d);
                 break;
@@ -468,132 +481,139 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
 // and keeps the first minimum: the same closest hit up to exact t ties).
+//
+// The walk is resumable: Trav holds its whole state, trace_step advances it by
+// one stack entry, so a lane whose walk ends can be shaded and handed its next
+// ray while the other lanes of its wave keep walking (rt_path_kernel).
 template <int TIER>
-__device__ bool trace(const SceneView& S, const Ray& wr, StackFor<TIER>& stk, const Rng& rng, HitInfo& hit, Diag& dg) {
-    constexpr bool FULL = TIER == TIER_FULL;
-    RT_DIAG_ONLY(unsigned long long it = 0;)
-    const double tmin = 1e-8;
-    const float tmin_f = f32_down(tmin);
-    Ray r = wr;
-    RayF rf = make_rayf(r);
-    double a = len2(r.d);
-    uint32_t xfs[MAX_XF];
-    uint32_t nxf = 0;
-    uint32_t sp = 0;
-    uint32_t cur = S.world_root;
+struct Trav {
+    Ray r;  // the ray in the frame of the innermost Transform entered (FULL only)
+    RayF rf;
+    double a;
     Closest cl;
-    cl.c = __builtin_huge_val();
-    cl.c_f = __builtin_huge_valf();
-    bool found = false;
-    auto record = [&](uint32_t ref, double t) {
-        found = true;
-        hit.t = t;
-        hit.ref = ref;
+    uint32_t cur, sp, nxf;
+    XfIds xfs;
+    bool found;
+    HitInfo hit;
+};
+
+template <int TIER>
+__device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, Trav<TIER>& T) {
+    T.r = wr;
+    T.rf = make_rayf(wr);
+    T.a = len2(wr.d);
+    T.cl.c = __builtin_huge_val();
+    T.cl.c_f = __builtin_huge_valf();
+    T.cur = S.world_root;
+    T.sp = 0;
+    T.nxf = 0;
+    T.found = false;
+    T.hit.nxf = 0;
+}
+
+// One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
+template <int TIER>
+__device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
+                                           const Rng& rng, Diag& dg) {
+    constexpr bool FULL = TIER == TIER_FULL;
+    constexpr double tmin = 1e-8;
+    const float tmin_f = f32_down(tmin);
+    if (T.cur == REF_NONE) {
+#ifdef RT_AB_FLAT_POP
+        if (T.sp == 0) return false;
+        --T.sp;
+        const uint2 e = stk.at(T.sp);
+        if (!(__uint_as_float(e.y) <= T.cl.c_f)) return true;  // culled entry: one empty step
+        T.cur = e.x;
+#else
+        T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+        if (T.cur == REF_NONE) return false;
+#endif
+    }
+    const Ray& r = FULL ? T.r : wr;
+    const uint32_t kind = ref_kind(T.cur), idx = ref_index(T.cur);
+    const uint32_t this_ref = T.cur;
+    T.cur = REF_NONE;
+    double t;
+    bool got = false;
+    auto record = [&](uint32_t ref, double tt) {
+        T.found = true;
+        T.hit.t = tt;
+        T.hit.ref = ref;
         if constexpr (FULL) {
-            hit.nxf = nxf;
-            for (uint32_t k = 0; k < MAX_XF; ++k) hit.xf[k] = k < nxf ? xfs[k] : 0u;
+            T.hit.nxf = T.nxf;
+            T.hit.xf = T.xfs;
         }
     };
-    for (;;) {
-#ifdef RT_AB_FLAT_POP
-        if (cur == REF_NONE) {
-            if (sp == 0) break;
-            --sp;
-            const uint2 e = stk.at(sp);
-            if (!(__uint_as_float(e.y) <= cl.c_f)) continue;  // culled entry: one empty iteration
-            cur = e.x;
+    RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
+    if (kind == K_BVH) {
+        T.cur = visit_node(S, idx, r, T.rf, T.a, tmin, tmin_f, T.cl, stk, T.sp, record);
+    } else if (kind == K_SPHERE) {
+        const double4 sp4 = S.spheres[idx];
+        got = sphere_t(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, tmin, T.cl.c, t);
+    } else if (kind == K_LIST) {
+        const uint32_t child = S.list_children[idx];
+        if (child != REF_NONE) {
+            if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+            T.cur = child;
         }
-#else
-        if (cur == REF_NONE) {
-            cur = pop(stk, sp, 0, cl.c_f);
-            if (cur == REF_NONE) break;
-        }
-#endif
-        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
-        const uint32_t this_ref = cur;
-        cur = REF_NONE;
-        double t;
-        bool got = false;
-        RT_DIAG_ONLY(++it; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
-        if (kind == K_BVH) {
-            cur = visit_node(S, idx, r, rf, a, tmin, tmin_f, cl, stk, sp, record);
-        } else if (kind == K_SPHERE) {
-            const double4 s = S.spheres[idx];
-            got = sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, cl.c, t);
-        } else if (kind == K_LIST) {
-            const uint32_t child = S.list_children[idx];
-            if (child != REF_NONE) {
-                if (S.list_children[idx + 1] != REF_NONE) stk.push(sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                cur = child;
+    } else if constexpr (TIER == TIER_MESH) {
+        if (kind == K_TRI || kind == K_QUAD) got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, T.cl.c, t);
+    } else if constexpr (FULL) {
+        switch (kind) {
+            case K_MSPHERE: {
+                const double4 s4 = S.msph_center[idx], m = S.msph_dir[idx];
+                const D3 cc = d3(s4.x, s4.y, s4.z) + r.time * d3(m.x, m.y, m.z);
+                got = sphere_t(cc, s4.w, r, T.a, tmin, T.cl.c, t);
+                break;
             }
-        } else if constexpr (TIER == TIER_MESH) {
-            if (kind == K_TRI || kind == K_QUAD) got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t);
-        } else if constexpr (FULL) {
-            switch (kind) {
-                case K_MSPHERE: {
-                    const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
-                    const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-                    got = sphere_t(cc, s.w, r, a, tmin, cl.c, t);
-                    break;
-                }
-                case K_QUAD:
-                case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t); break;
-                case K_XFORM: {
-                    const DXform& X = S.xforms[idx];
-                    stk.push(sp++, make_ref(K_POPXF, 0), NO_CULL);
-                    xfs[nxf++] = idx;
-                    r = xf_ray(X, r);
-                    rf = make_rayf(r);
-                    a = len2(r.d);
-                    cur = X.child;
-                    break;
-                }
-                case K_POPXF: {
-                    --nxf;
-                    r = wr;
-                    for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs[k]], r);
-                    rf = make_rayf(r);
-                    a = len2(r.d);
-                    break;
-                }
-                case K_MEDIUM: {
-                    // volume.rs:37-73
-                    const DMedium M = S.media[idx];
-                    double t1, t2;
-                    const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
-                    if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, sp, t1)) break;
-                    if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, sp, t2)) break;
-                    if (t1 < tmin) t1 = tmin;
-                    if (t2 > cl.c) t2 = cl.c;
-                    if (t1 >= t2) break;
-                    if (t1 < 0.0) t1 = 0.0;
-                    const double ray_length = len(r.d);
-                    const double inside = (t2 - t1) * ray_length;
-                    const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
-                    if (hd > inside) break;
-                    t = t1 + hd / ray_length;  // volume.rs:65
-                    got = t <= cl.c;
-                    break;
-                }
-                default: break;
+            case K_QUAD:
+            case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, T.cl.c, t); break;
+            case K_XFORM: {
+                const DXform& X = S.xforms[idx];
+                stk.push(T.sp++, make_ref(K_POPXF, 0), NO_CULL);
+                T.xfs.set(T.nxf++, idx);
+                T.r = xf_ray(X, T.r);
+                T.rf = make_rayf(T.r);
+                T.a = len2(T.r.d);
+                T.cur = X.child;
+                break;
             }
-        }
-        if (got) {
-            cl.set(t);
-            record(this_ref, t);
+            case K_POPXF: {
+                --T.nxf;
+                T.r = wr;
+                for (uint32_t k = 0; k < T.nxf; ++k) T.r = xf_ray(S.xforms[T.xfs.get(k)], T.r);
+                T.rf = make_rayf(T.r);
+                T.a = len2(T.r.d);
+                break;
+            }
+            case K_MEDIUM: {
+                // volume.rs:37-73
+                const DMedium M = S.media[idx];
+                double t1, t2;
+                const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
+                if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, T.sp, t1)) break;
+                if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, T.sp, t2)) break;
+                if (t1 < tmin) t1 = tmin;
+                if (t2 > T.cl.c) t2 = T.cl.c;
+                if (t1 >= t2) break;
+                if (t1 < 0.0) t1 = 0.0;
+                const double ray_length = len(r.d);
+                const double inside = (t2 - t1) * ray_length;
+                const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
+                if (hd > inside) break;
+                t = t1 + hd / ray_length;  // volume.rs:65
+                got = t <= T.cl.c;
+                break;
+            }
+            default: break;
         }
     }
-    if constexpr (!FULL) hit.nxf = 0;
-#ifdef RT_DIAG
-    dg.lane_trace_iters += it;
-    unsigned long long m = it;
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(m, off);
-        m = o > m ? o : m;
+    if (got) {
+        T.cl.set(t);
+        record(this_ref, t);
     }
-    dg.wave_trace_iters += m;
-#endif
-    return found;
+    return true;
 }
 
 // ------------------------------------------------------------------ hit record
@@ -611,7 +631,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     constexpr bool FULL = TIER == TIER_FULL, PLANAR = TIER >= TIER_MESH;
     Ray r = wr;
     if constexpr (FULL)
-        for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf[k]], r);
+        for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf.get(k)], r);
     const uint32_t kind = ref_kind(h.ref), idx = ref_index(h.ref);
     Rec rec;
     rec.u = 0.0;
@@ -655,13 +675,14 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     rec.front = dot(r.d, outward) < 0.0;
     rec.n = rec.front ? outward : -outward;
     rec.p = p;
-    if constexpr (FULL)
+    if constexpr (FULL) {
         for (int k = (int)h.nxf - 1; k >= 0; --k) {
-            const DXform& X = S.xforms[h.xf[k]];
+            const DXform& X = S.xforms[h.xf.get(k)];
             rec.p = xf_out(X, rec.p);
             bool ok;
             rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
         }
+    }
     if constexpr (PLANAR) {
         // RemappedMaterial::remap_record (obj.rs:32-62), no normal map: applied to
         // the record every material of an OBJ triangle sees (scatter and emitted)
@@ -678,6 +699,19 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
                 bool ok;
                 rec.n = unit(nm, ok);
                 if (!ok) panic = true;  // .unwrap() (obj.rs:40)
+                if constexpr (FULL) {
+                    if (R.normal_tex >= 0) {  // obj.rs:42-51
+                        if (!R.uv_ok) panic = true;  // u_vec.unwrap()
+                        const DRemapNM& F = S.remap_nm[ri];
+                        const D3 c = tex_value<FULL>(S, R.normal_tex, tu, tv, rec.p);
+                        const D3 nc = 2.0 * c - d3(1.0, 1.0, 1.0);
+                        const D3 raw = ((nc.x * d3(F.u_vec[0], F.u_vec[1], F.u_vec[2])) +
+                                        (nc.y * d3(F.v_vec[0], F.v_vec[1], F.v_vec[2]))) + (nc.z * rec.n);
+                        bool ok2;
+                        rec.n = unit(raw, ok2);
+                        if (!ok2) panic = true;  // "The mapped normal can't normalized!"
+                    }
+                }
                 rec.u = tu;
                 rec.v = tv;
             }
@@ -776,14 +810,10 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
 template <int TIER>
-__device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, StackFor<TIER>& stk,
-                                       bool& panic, Diag& dg) {
+__device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
+                                      const HitInfo& h, bool& panic) {
     constexpr bool FULL = TIER == TIER_FULL;
     uint32_t ovf = 0;
-    HitInfo h;
-    RT_DIAG_ONLY(const unsigned long long t_tr0 = __builtin_amdgcn_s_memtime();)
-    const bool hit_any = trace<TIER>(S, ray, stk, rng, h, dg);
-    RT_DIAG_ONLY(const unsigned long long t_tr1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_tr1 - t_tr0;)
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
         if (S.background_tex >= 0) {
@@ -948,6 +978,22 @@ __device__ __forceinline__ bool bounce(const SceneView& S, Ray& ray, D3& beta, D
 #ifndef RT_BASIC_WAVES
 #define RT_BASIC_WAVES 4  // waves per SIMD the basic tier is register-allocated for
 #endif
+#ifndef RT_FULL_WAVES
+#define RT_FULL_WAVES 3  // 3 waves with some spills beat 2 without: C3 -13 %, C5 -19 %
+#endif
+// Lanes of a wave that must have finished their walk before it shades (64 =
+// all).  Trace-heavy worlds (deep triangle BVHs) gain from shading in batches;
+// for C2 the shading divergence of small batches costs more than the walks
+// gain (A/B in DESIGN.md).
+#ifndef RT_SHADE_BATCH_BASIC
+#define RT_SHADE_BATCH_BASIC 64
+#endif
+#ifndef RT_SHADE_BATCH_MESH
+#define RT_SHADE_BATCH_MESH 48
+#endif
+#ifndef RT_SHADE_BATCH_FULL
+#define RT_SHADE_BATCH_FULL 64
+#endif
 #ifndef RT_MESH_WAVES
 #define RT_MESH_WAVES 4  // 4-wave budget (some spills) beats 2 waves: 164.7 vs 263.8 ms (C4, 64 spp)
 #endif
@@ -960,11 +1006,11 @@ struct KParams {
     uint32_t* queue;
     double* partial;
     unsigned long long* stats;
-    RT_GLOBAL uint2* stack_ovf;  // mesh tier: [stack_need - RT_STACK_MESH][grid * RT_BLOCK] entries
+    RT_GLOBAL uint2* stack_ovf;  // mesh / full tiers: [stack_need - LDS entries][grid * RT_BLOCK]
 };
 
 template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
@@ -988,6 +1034,8 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIE
     uint32_t n_rays = 0, n_panics = 0;
 
     Diag dg;
+    Trav<TIER> T;
+    bool walking = false;
     for (;;) {
         RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
         // ---- refill: wave-aggregated dequeue of stratum rows
@@ -1038,14 +1086,39 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIE
             in_path = true;
         }
 
-        // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
-        rng.begin(vertex);
-        ++n_rays;
+        // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1:
+        // world.hit as a resumable walk.  The wave walks until RT_SHADE_BATCH of its
+        // lanes have finished (or none walks any more); those are shaded and get
+        // their next ray while the unfinished walks carry over to the next round,
+        // so short walks do not idle behind the longest one of the wave.
+        if (!walking) {
+            rng.begin(vertex);
+            ++n_rays;
+            trace_begin<TIER>(S, ray, T);
+            walking = true;
+        }
+        RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
+        constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
+                            : (TIER == TIER_MESH ? RT_SHADE_BATCH_MESH : RT_SHADE_BATCH_FULL);
+        if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
+            while (walking) {
+                RT_DIAG_ONLY(++dg.wave_trace_iters;)
+                walking = trace_step<TIER>(S, ray, T, stk, rng, dg);
+            }
+        } else {
+            const unsigned long long active = __ballot(true);
+            for (;;) {
+                RT_DIAG_ONLY(++dg.wave_trace_iters;)
+                if (walking) walking = trace_step<TIER>(S, ray, T, stk, rng, dg);
+                const unsigned long long w = __ballot(walking);
+                if (w == 0 || __popcll(active & ~w) >= BATCH) break;
+            }
+        }
+        RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
+        if (BATCH < 64 && walking) continue;
         bool panic = false;
-        RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;
-                     const unsigned long long trace_before = dg.cyc_trace;)
-        bool end_path = bounce<TIER>(S, ray, beta, L, rng, stk, panic, dg);
-        RT_DIAG_ONLY(dg.cyc_shade += (__builtin_amdgcn_s_memtime() - t_b0) - (dg.cyc_trace - trace_before);)
+        bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic);
+        RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_b1;)
         if (panic) {
             ++n_panics;
             end_path = true;
@@ -1089,10 +1162,62 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? 2 : (TIER == TIE
     if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
 }
 
+}  // namespace rtk
+
+// ------------------------------------------------------------------ host launchers
+// The product library compiles this file once per kernel tier (-DRT_TIER_ONLY=N,
+// each with its own code-generation flags, raytracer-2025_amd/Makefile) plus
+// once for the common part (-DRT_COMMON_ONLY); diagnostic / A-B builds compile
+// it whole.
+#define RT_TIER_ENTRY(N)                                                                                        \
+    extern "C" hipError_t rtk_launch_path_##N(int grid, hipStream_t stream, const rtk::KParams* P) {          \
+        hipLaunchKernelGGL(rtk::rt_path_kernel<N>, dim3(grid), dim3(RT_BLOCK), 0, stream, P);               \
+        return hipGetLastError();                                                                            \
+    }                                                                                                        \
+    extern "C" int rtk_occupancy_##N(int* blocks_per_cu) {                                                   \
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<N>, RT_BLOCK, 0); \
+    }
+#if !defined(RT_COMMON_ONLY)
+#if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 0
+RT_TIER_ENTRY(0)
+#endif
+#if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 1
+RT_TIER_ENTRY(1)
+#endif
+#if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 2
+RT_TIER_ENTRY(2)
+#endif
+#endif
+
+#if !defined(RT_TIER_ONLY)
+extern "C" hipError_t rtk_launch_path_0(int, hipStream_t, const rtk::KParams*);
+extern "C" hipError_t rtk_launch_path_1(int, hipStream_t, const rtk::KParams*);
+extern "C" hipError_t rtk_launch_path_2(int, hipStream_t, const rtk::KParams*);
+extern "C" int rtk_occupancy_0(int*);
+extern "C" int rtk_occupancy_1(int*);
+extern "C" int rtk_occupancy_2(int*);
+
+namespace rtk {
+// Color::to_rgb (utils/color.rs:14-36): optional ACES fit, clamp, then the sRGB
+// OETF and f64 -> u8 (palette restated as in oracle/rt_oracle.cpp to_rgb;
+// parity unpinned).  No contraction, so the arithmetic is the host's.
+__device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
+#pragma clang fp contract(off)
+    if (toon == 1) {
+        const double m = (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14);
+        x = m < 0.0 ? 0.0 : (m > 1.0 ? 1.0 : m);
+    }
+    const double sv = x <= 0.0031308 ? 12.92 * x : 1.055 * pow(x, 1.0 / 2.4) - 0.055;
+    const double q = round(sv * 255.0);
+    return (uint8_t)(q < 0.0 ? 0.0 : (q > 255.0 ? 255.0 : q));
+}
+
 // Sums the S stratum rows of each pixel in s_i order, * pixel_sample_scale,
-// to linear f32 (camera.rs:193).
+// to linear f32 (camera.rs:193), and -- when srgb is given -- the pixel's
+// to_rgb bytes from the f64 sum, as the reference converts its f64 color.
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
-                                                       double scale, float* __restrict__ out) {
+                                                       double scale, float* __restrict__ out,
+                                                       uint8_t* __restrict__ srgb, int toon) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
     const double* src = partial + (uint64_t)p * S * 3;
@@ -1105,25 +1230,38 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     out[(uint64_t)p * 3 + 0] = (float)(r * scale);
     out[(uint64_t)p * 3 + 1] = (float)(g * scale);
     out[(uint64_t)p * 3 + 2] = (float)(b * scale);
+    if (srgb) {
+        srgb[(uint64_t)p * 3 + 0] = srgb_u8(r * scale, toon);
+        srgb[(uint64_t)p * 3 + 1] = srgb_u8(g * scale, toon);
+        srgb[(uint64_t)p * 3 + 2] = srgb_u8(b * scale, toon);
+    }
 }
 
+// to_rgb of a linear f32 framebuffer already on the device (e.g. the gathered
+// multi-GPU frame).
+__global__ void __launch_bounds__(256) rt_to_rgb_kernel(const float* __restrict__ lin, uint8_t* __restrict__ srgb,
+                                                       uint64_t n, int toon) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) srgb[i] = srgb_u8((double)lin[i], toon);
+}
 }  // namespace rtk
 
-// ------------------------------------------------------------------ host launchers
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
-    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL;
-    if ((features & full) || stack_need > RT_STACK_MESH_MAX) return rtk::TIER_FULL;
+    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL |
+                          rtk::F_NORMALMAP;
+    if (features & full) return rtk::TIER_FULL;
     if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;
 }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
-    return tier == rtk::TIER_FULL ? RT_STACK_FULL : (tier == rtk::TIER_MESH ? RT_STACK_MESH_MAX : RT_STACK_BASIC);
+    return tier == rtk::TIER_BASIC ? RT_STACK_BASIC : RT_STACK_MAX;
 }
 
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
-                                       double* partial, unsigned long long* stats, float* out, hipStream_t stream,
-                                       int tier, int grid, void* params_dev, void* stack_ovf) {
+                                       double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
+                                       int toon, hipStream_t stream, int tier, int grid, void* params_dev,
+                                       void* stack_ovf) {
     rtk::KParams K;
     K.S = *view;
     rtk::Frame& F = K.F;
@@ -1155,18 +1293,20 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
-    if (tier == rtk::TIER_BASIC)
-        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_BASIC>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
-    else if (tier == rtk::TIER_MESH)
-        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_MESH>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
-    else
-        hipLaunchKernelGGL(rtk::rt_path_kernel<rtk::TIER_FULL>, dim3(grid), dim3(RT_BLOCK), 0, stream, (const rtk::KParams*)Pd);
-    e = hipGetLastError();
+    e = tier == rtk::TIER_BASIC  ? rtk_launch_path_0(grid, stream, Pd)
+        : tier == rtk::TIER_MESH ? rtk_launch_path_1(grid, stream, Pd)
+                                 : rtk_launch_path_2(grid, stream, Pd);
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
-                       fd->pixel_sample_scale, out);
+                       fd->pixel_sample_scale, out, srgb, toon);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rtk::rt_to_rgb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, lin, srgb, n, toon);
     return hipGetLastError();
 }
 
@@ -1184,9 +1324,8 @@ extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
 #endif
 
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
-    if (tier == rtk::TIER_BASIC)
-        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_BASIC>, RT_BLOCK, 0);
-    if (tier == rtk::TIER_MESH)
-        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_MESH>, RT_BLOCK, 0);
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<rtk::TIER_FULL>, RT_BLOCK, 0);
+    return tier == rtk::TIER_BASIC  ? rtk_occupancy_0(blocks_per_cu)
+         : tier == rtk::TIER_MESH ? rtk_occupancy_1(blocks_per_cu)
+                                  : rtk_occupancy_2(blocks_per_cu);
 }
+#endif  // !RT_TIER_ONLY

@@ -87,9 +87,14 @@ struct alignas(16) DPlanar {
 struct alignas(16) DRemap {
     double n[9];
     double tex_ori[2], tex_u[2], tex_v[2];
-    double pad;
+    int32_t normal_tex;  // -1 = no normal map; else texture id (remap_nm holds the frame)
+    int32_t uv_ok;       // uv_local_to_world gave Some(u_vec), Some(v_vec)
 };
 static_assert(sizeof(DRemap) == 128, "DRemap must be 128 B");
+// The tangent frame of a normal-mapped OBJ triangle (obj.rs:44-50, 196-210).
+struct alignas(16) DRemapNM {
+    double u_vec[3], v_vec[3];
+};
 
 // Transform (shapes.rs:23-29).  Rotation kept as the quaternion the reference
 // uses plus its 3x3 matrix form (the kernel rotates with the matrix).
@@ -172,6 +177,7 @@ struct SceneView {
     const RT_GLOBAL int32_t* planar_mat;
     const RT_GLOBAL int32_t* planar_remap;   // index into remaps, -1 = plain Triangle/Quad
     const RT_GLOBAL DRemap* remaps;
+    const RT_GLOBAL DRemapNM* remap_nm;
     const RT_GLOBAL uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
     const RT_GLOBAL DXform* xforms;
     const RT_GLOBAL DMedium* media;
@@ -196,6 +202,7 @@ enum : uint32_t {
     F_TEXFULL = 32u,  // image / noise textures
     F_MATFULL = 64u,  // DiffuseLight, Isotropic, Transparent, Mix
     F_REMAP = 128u,   // OBJ triangles with RemappedMaterial
+    F_NORMALMAP = 256u,  // ... with a normal map (full tier: image textures)
 };
 
 }  // namespace rtk

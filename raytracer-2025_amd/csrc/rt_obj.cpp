@@ -235,10 +235,8 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
 
         if (mtl_failed) mtls.clear();
         // load_materials (obj.rs:212-345)
-        std::vector<int32_t> mats;
+        std::vector<int32_t> mats, normal_maps;
         for (const MtlRec& m : mtls) {
-            if (!m.normal_texture.empty())
-                return set_error(RT_EUNSUPPORTED, "normal maps (RemappedMaterial::normal_tex) are not on the kernel path");
             int32_t base_tex;
             if (!m.diffuse_texture.empty()) {
                 if (file_exists(dir + "/" + m.diffuse_texture))
@@ -277,6 +275,22 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
             if (m.has_dissolve && m.dissolve < 1.0) mat = rt_mat_mix(s, rt_mat_transparent(s), mat, m.dissolve);
             if (mat < 0) return mat;
             mats.push_back(mat);
+            // normal map (obj.rs:324-343): "file" or "-bm <scale> file" -> prefix/file,
+            // ImageTexture::new_raw_image; a missing file reads as cyan
+            int32_t ntex = -1;
+            if (!m.normal_texture.empty()) {
+                std::string name = m.normal_texture;
+                if (name.compare(0, 3, "-bm") == 0) {
+                    std::istringstream is(name.substr(3));
+                    std::string part, last;
+                    while (is >> part) last = part;
+                    if (!last.empty()) name = last;
+                }
+                if (file_exists(dir + "/" + name))
+                    return set_error(RT_EUNSUPPORTED, "normal-map images must be decoded by the caller (rt_tex_image)");
+                ntex = rt_tex_image(s, 0, 0, nullptr, 0);
+            }
+            normal_maps.push_back(ntex);
         }
 
         int32_t objs = rt_hittables_new(s);
@@ -317,6 +331,20 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
                 o.tex_u[1] = tc[1][1] - tc[0][1];
                 o.tex_v[0] = tc[2][0] - tc[0][0];
                 o.tex_v[1] = tc[2][1] - tc[0][1];
+                o.normal_tex = normal_maps[mi];
+                if (o.normal_tex >= 0) {
+                    // uv_local_to_world (obj.rs:196-210)
+                    const double tux = o.tex_u[0], tuy = o.tex_u[1], tvx = o.tex_v[0], tvy = o.tex_v[1];
+                    const double ua = tvy / (-tuy * tvx + tux * tvy);
+                    const double ub = tuy / (tuy * tvx - tux * tvy);
+                    const double va = tvx / (tuy * tvx - tux * tvy);
+                    const double vb = tux / (-tuy * tvx + tux * tvy);
+                    const V3 uw = ua * wu + ub * wv, vw = va * wu + vb * wv;
+                    const V3 un = div(uw, length(uw)), vn = div(vw, length(vw));
+                    o.uv_ok = finite(un) && finite(vn);  // else .unwrap() panics when shaded
+                    o.u_vec = un;
+                    o.v_vec = vn;
+                }
                 rt_hittables_add(s, list, tri);
                 ++added;
             }

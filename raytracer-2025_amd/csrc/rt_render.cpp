@@ -27,6 +27,8 @@ struct DeviceWorld {
     size_t partial_bytes = 0;
     float* out = nullptr;
     size_t out_bytes = 0;
+    uint8_t* srgb = nullptr;  // to_rgb bytes of the host-path render
+    size_t srgb_bytes = 0;
     void* stack_ovf = nullptr;  // mesh tier: traversal-stack entries beyond the LDS part
     size_t stack_ovf_bytes = 0;
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
@@ -51,6 +53,7 @@ void destroy_device_world(DeviceWorld* d) {
     if (d->partial) (void)hipFree(d->partial);
     if (d->out) (void)hipFree(d->out);
     if (d->stack_ovf) (void)hipFree(d->stack_ovf);
+    if (d->srgb) (void)hipFree(d->srgb);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
     delete d;
@@ -114,8 +117,9 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
                                         std::to_string(stack_cap));
-    if (tier == rtk::TIER_MESH && hw.stack_need > RT_STACK_MESH) {
-        const size_t need = (size_t)(hw.stack_need - RT_STACK_MESH) * d->grid[tier] * RT_BLOCK * sizeof(uint64_t);
+    const uint32_t lds_entries = tier == rtk::TIER_BASIC ? RT_STACK_BASIC : (tier == rtk::TIER_MESH ? RT_STACK_MESH : RT_STACK_FULL);
+    if (hw.stack_need > lds_entries) {
+        const size_t need = (size_t)(hw.stack_need - lds_entries) * d->grid[tier] * RT_BLOCK * sizeof(uint64_t);
         if (need > d->stack_ovf_bytes) {
             if (d->stack_ovf) (void)hipFree(d->stack_ovf);
             d->stack_ovf = nullptr;
@@ -129,6 +133,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
            o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
            o_pl = put(blob, hw.planars), o_pla = put(blob, hw.planar_area), o_plm = put(blob, hw.planar_mat),
            o_plr = put(blob, hw.planar_remap), o_rm = put(blob, hw.remaps),
+           o_rnm = put(blob, (hw.features & rtk::F_NORMALMAP) ? hw.remap_nm : std::vector<rtk::DRemapNM>()),
            o_lc = put(blob, hw.list_children), o_xf = put(blob, hw.xforms), o_md = put(blob, hw.media),
            o_mat = put(blob, hw.materials), o_tex = put(blob, hw.textures), o_tx = put(blob, hw.texels),
            o_per = put(blob, hw.perlin);
@@ -152,6 +157,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     v.planar_mat = (const int32_t*)(b + o_plm);
     v.planar_remap = (const int32_t*)(b + o_plr);
     v.remaps = (const rtk::DRemap*)(b + o_rm);
+    v.remap_nm = (const rtk::DRemapNM*)(b + o_rnm);
     v.list_children = (const uint32_t*)(b + o_lc);
     v.xforms = (const rtk::DXform*)(b + o_xf);
     v.media = (const rtk::DMedium*)(b + o_md);
@@ -246,19 +252,8 @@ static int32_t ensure_buffers(DeviceWorld* d, const rtk_frame_desc& f, bool need
     return RT_OK;
 }
 
-// sRGB OETF + u8 (utils/color.rs:14-36; palette restated, parity unpinned)
-static uint8_t srgb_u8(double x, int toon) {
-    if (toon == 1) {
-        double m = (x * (2.51 * x + 0.03)) / (x * (2.43 * x + 0.59) + 0.14);
-        x = std::clamp(m, 0.0, 1.0);
-    }
-    double s = x <= 0.0031308 ? 12.92 * x : 1.055 * std::pow(x, 1.0 / 2.4) - 0.055;
-    double q = std::round(s * 255.0);
-    return (uint8_t)std::clamp(q, 0.0, 255.0);
-}
-
 static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
-                      float* dev_out, hipStream_t stream) {
+                      float* dev_out, hipStream_t stream, bool want_srgb = false) {
     if (!s) return set_error(RT_EINVAL, "null scene");
     if (world < 0 || (size_t)world >= s->objs.size() || s->objs[world].hidden)
         return set_error(RT_EHANDLE, "unknown world handle");
@@ -287,8 +282,20 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     float* out = dev_out ? dev_out : d->out;
     const bool run = f.rows > 0 && f.max_depth > 0;
     if (run) {
-        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, stream, d->tier, d->grid[d->tier], d->params,
-                             d->stack_ovf);
+        uint8_t* srgb = nullptr;
+        if (want_srgb) {
+            const size_t nb = (size_t)f.W * f.rows * 3;
+            if (nb > d->srgb_bytes) {
+                if (d->srgb) (void)hipFree(d->srgb);
+                d->srgb = nullptr;
+                d->srgb_bytes = 0;
+                if ((e = hipMalloc(&d->srgb, nb)) != hipSuccess) return hip_fail(e, "hipMalloc srgb");
+                d->srgb_bytes = nb;
+            }
+            srgb = d->srgb;
+        }
+        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, stream, d->tier,
+                             d->grid[d->tier], d->params, d->stack_ovf);
         if (e != hipSuccess) return hip_fail(e, "kernel launch");
     } else if (f.rows > 0) {
         // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)
@@ -371,25 +378,35 @@ int32_t rt_render_device_wait(rt_scene* s, rt_stats* st) {
     return wait(s, st);
 }
 
+int32_t rt_to_rgb_device(const float* lin_dev, uint8_t* srgb_dev, uint64_t n_values, int32_t toon_map, void* stream) {
+    if (n_values && (!lin_dev || !srgb_dev)) return set_error(RT_EINVAL, "null argument");
+    hipError_t e = rtk_launch_to_rgb(lin_dev, srgb_dev, n_values, toon_map, (hipStream_t)stream);
+    return e == hipSuccess ? RT_OK : hip_fail(e, "to_rgb launch");
+}
+
 int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
                   float* out_lin, uint8_t* out_srgb, rt_stats* st) {
     try {
         hipStream_t stream = opts ? (hipStream_t)opts->stream : nullptr;
-        int32_t rc = launch(s, world, lights, cam, opts, nullptr, stream);
-        if (rc != RT_OK) return rc;
-        DeviceWorld* d = s->dev;
         const uint32_t rows = rt_shard_rows(cam, opts);
         const size_t n = (size_t)cam->image_width * rows * 3;
-        std::vector<float> host(n);
+        const bool srgb_dev = out_srgb && cam->max_depth > 0;  // else every pixel is BLACK -> 0
+        int32_t rc = launch(s, world, lights, cam, opts, nullptr, stream, srgb_dev);
+        if (rc != RT_OK) return rc;
+        DeviceWorld* d = s->dev;
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return hip_fail(e, "render");
-        if (n && (e = hipMemcpy(host.data(), d->out, n * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
+        if (n && out_lin && (e = hipMemcpy(out_lin, d->out, n * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
             return hip_fail(e, "hipMemcpy output");
-        int32_t wrc = wait(s, st);
-        if (out_lin) std::memcpy(out_lin, host.data(), n * sizeof(float));
-        if (out_srgb)
-            for (size_t i = 0; i < n; ++i) out_srgb[i] = srgb_u8(host[i], cam->toon_map);
-        return wrc;
+        if (n && out_srgb) {
+            if (srgb_dev) {
+                if ((e = hipMemcpy(out_srgb, d->srgb, n, hipMemcpyDeviceToHost)) != hipSuccess)
+                    return hip_fail(e, "hipMemcpy srgb");
+            } else {
+                std::memset(out_srgb, 0, n);
+            }
+        }
+        return wait(s, st);
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }

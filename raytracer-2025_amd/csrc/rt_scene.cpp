@@ -375,8 +375,17 @@ struct Flattener {
                         rm.tex_u[j] = o.tex_u[j];
                         rm.tex_v[j] = o.tex_v[j];
                     }
+                    rm.normal_tex = o.normal_tex;
+                    rm.uv_ok = o.uv_ok ? 1 : 0;
+                    rtk::DRemapNM nm{};
+                    if (o.normal_tex >= 0) {
+                        nm.u_vec[0] = o.u_vec.x; nm.u_vec[1] = o.u_vec.y; nm.u_vec[2] = o.u_vec.z;
+                        nm.v_vec[0] = o.v_vec.x; nm.v_vec[1] = o.v_vec.y; nm.v_vec[2] = o.v_vec.z;
+                        out.features |= rtk::F_NORMALMAP;
+                    }
                     out.planar_remap.push_back((int32_t)out.remaps.size());
                     out.remaps.push_back(rm);
+                    out.remap_nm.push_back(nm);
                     out.features |= rtk::F_REMAP;
                 } else {
                     out.planar_remap.push_back(-1);
@@ -597,6 +606,7 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         }
     };
     use_tex(background_tex);
+    for (const auto& rm : out.remaps) use_tex(rm.normal_tex);
     for (size_t i = 0; i < out.materials.size(); ++i)
         if (mat_used[i]) use_tex(out.materials[i].tex);
     while (!twork.empty()) {

@@ -74,6 +74,9 @@ struct Obj {
     bool remap = false;
     V3 rn[3];
     double tex_ori[2] = {0, 0}, tex_u[2] = {0, 0}, tex_v[2] = {0, 0};
+    int normal_tex = -1;  // RemappedMaterial::normal_tex (raw image texture), -1 = None
+    bool uv_ok = false;   // u_vec / v_vec are Some
+    V3 u_vec, v_vec;
     // list / bvh / transform / medium
     std::vector<int> children;
     int left = -1, right = -1, child = -1;
@@ -113,6 +116,7 @@ struct HostWorld {
     std::vector<int32_t> planar_mat;
     std::vector<int32_t> planar_remap;
     std::vector<rtk::DRemap> remaps;
+    std::vector<rtk::DRemapNM> remap_nm;  // parallel to remaps when any normal map is used
     std::vector<uint32_t> list_children;
     std::vector<rtk::DXform> xforms;
     std::vector<rtk::DMedium> media;

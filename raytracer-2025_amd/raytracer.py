@@ -198,6 +198,23 @@ class Camera:
         self.focus_distance = 10.0
         self.toon_map = 0  # ToonMap::None
 
+    @staticmethod
+    def from_json(api, path):
+        """Camera::from_json (camera.rs:119-159): the CameraParams fields from a
+        JSON file over Camera::default (path given directly)."""
+        c = RtCamera()
+        api.check(api.camera_from_json(os.fsencode(path), C.byref(c)))
+        cam = Camera()
+        cam.aspect_ratio = c.aspect_ratio
+        cam.image_width = c.image_width
+        cam.vertical_fov_in_degrees = c.vertical_fov_in_degrees
+        cam.look_from = tuple(c.look_from)
+        cam.look_at = tuple(c.look_at)
+        cam.vec_up = tuple(c.vec_up)
+        cam.defocus_angle_in_degrees = c.defocus_angle_in_degrees
+        cam.focus_distance = c.focus_distance
+        return cam
+
     def to_c(self):
         c = RtCamera()
         c.aspect_ratio = float(self.aspect_ratio)
@@ -249,3 +266,10 @@ class Camera:
                         srgb.ctypes.data_as(C.POINTER(C.c_uint8)) if srgb is not None else None, C.byref(stats))
         api.check(rc)
         return lin, srgb, stats
+
+
+def save_png(api, path, srgb):
+    """img.save(path) after create_dir_all (main.rs:39-47): srgb is HxWx3 u8."""
+    a = np.ascontiguousarray(srgb, dtype=np.uint8)
+    h, w = a.shape[:2]
+    api.check(api.write_png(os.fsencode(path), w, h, a.ctypes.data_as(C.c_void_p)))

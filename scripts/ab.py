@@ -3,7 +3,7 @@
 by `make -C raytracer-2025_amd ab`) in one process on the C2 scene: each
 variant renders the same frame; path-kernel time from the library's HIP
 events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]
-AB_WORKLOAD=c4 renders the C4 1M-triangle terrain instead of C2."""
+AB_WORKLOAD=c3|c4|c5 renders that config's scene (C5 at 1920 wide) instead of C2."""
 import ctypes
 import glob
 import importlib
@@ -28,7 +28,12 @@ runs = {}
 for n in names:
     api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", f"librt_ab_{n}.so")), "rt_")
     scene = rt.Scene(api)
-    if os.environ.get("AB_WORKLOAD", "c2") == "c4":
+    wl = os.environ.get("AB_WORKLOAD", "c2")
+    if wl == "c3":
+        world, lights, cam = scenes.cornell_smoke(scene, 800, spp)
+    elif wl == "c5":
+        world, lights, cam = scenes.final_scene(scene, 1920, spp, 40, aspect_ratio=16 / 9)
+    elif wl == "c4":
         import tempfile
         obj = os.path.join(tempfile.gettempdir(), "rt_terrain_707", "terrain.obj")
         if not os.path.exists(obj):

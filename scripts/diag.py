@@ -23,7 +23,15 @@ api = capi.Api(lib, "rt_")
 lib.rt_diag_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 scene = rt.Scene(api)
-world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+wl = os.environ.get("AB_WORKLOAD", "c2")
+if wl == "c4":
+    import tempfile
+    obj = os.path.join(tempfile.gettempdir(), "rt_terrain_707", "terrain.obj")
+    if not os.path.exists(obj):
+        scenes.write_terrain_obj(os.path.dirname(obj), 707)
+    world, lights, cam = scenes.obj_terrain(scene, obj, 1920, spp)
+else:
+    world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
 buf = (ctypes.c_ulonglong * 16)()
 lib.rt_diag_counters(buf, 1)
@@ -32,7 +40,7 @@ lib.rt_diag_counters(buf, 0)
 c = list(buf)
 tot = c[0] + c[1] + c[2]
 out = {
-    "spp": spp,
+    "workload": wl, "spp": spp,
     "kernel_ms": st.kernel_ms,
     "samples": st.samples,
     "rays": st.rays,

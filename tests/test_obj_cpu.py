@@ -223,3 +223,56 @@ def test_terrain_loads_on_both(product, oracle, rt, capi, scenes, tmp_path):
     w, _, cam = scenes.obj_terrain(so, p, 32, 4)
     lin, _, st = cam.render(w, None, seed=1)
     assert st.panics == 0 and np.isfinite(lin).all() and lin.mean() > 0.05
+
+
+REF_ASSETS = "/root/reference/assets/Final"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_ASSETS), reason="reference assets not present (GPU box)")
+@pytest.mark.parametrize("name,tier", [("镜子.obj", 2), ("水面.obj", 2)])
+def test_reference_vanilla_assets_load(product, oracle, rt, capi, name, tier):
+    """The two OBJs the reference's obj_scene loads with vanilla_material = true
+    (main.rs:213, 217): the mirror (Pm 1 -> Metal, Ke 0 0 0 -> DiffuseLight
+    around it) and the water (Tf 1 -> Dielectric, map_Bump "-bm 1 file" whose
+    file is absent -> cyan normal map).  Read in place, not copied."""
+    path = os.path.join(REF_ASSETS, name)
+    s, w = load(product, rt, path)
+    info = prims(product, capi, s, w)
+    assert info.primitives == 2 and info.kernel_tier == tier
+    so, wo = load(oracle, rt, path)
+    cam = rt.Camera()
+    cam.image_width = 24
+    cam.samples_per_pixel = 4
+    cam.max_depth = 6
+    cam.look_from = (0.0, 3.0, 2.0)
+    cam.look_at = (-1.5, 2.5, -13.0)
+    cam.background = so.SkyGradient((1.0, 1.0, 1.0), (0.5, 0.7, 1.0))
+    world = so.Hittables()
+    world.add(wo)
+    lin, _, st = cam.render(world, None, seed=1)
+    assert np.isfinite(lin).all()
+
+
+NM_MTL = "newmtl water\nKd 1 1 1\nNi 1.33\nTf 1.0 1.0 1.0\nmap_Bump -bm 1.000000 absent_normal.png\n"
+
+
+def test_missing_normal_map_is_cyan(product, oracle, rt, capi, tmp_path):
+    """normal_color = cyan*2 - 1 = (-1, 1, 1): the shading normal tilts to
+    -u_vec + v_vec + n (obj.rs:42-51); the oracle image must differ from the
+    same quad without the map, and the product must pick the full tier."""
+    obj = QUAD.format(mat="water")
+    p_nm = write(tmp_path, obj, mtl=NM_MTL, name="nm.obj")
+    s, w = load(product, rt, p_nm)
+    info = prims(product, capi, s, w)
+    assert info.kernel_tier == 2 and info.features & 256  # F_NORMALMAP
+    a = _render_oracle(oracle, rt, lambda so: _wrap(so, p_nm))
+    (tmp_path / "plain").mkdir()
+    p_plain = write(tmp_path / "plain", obj, mtl=NM_MTL.split("map_Bump")[0], name="plain.obj")
+    b = _render_oracle(oracle, rt, lambda so: _wrap(so, p_plain))
+    assert np.abs(a - b).max() > 1e-3
+
+
+def _wrap(s, path):
+    w = s.Hittables()
+    w.add(s.Wavefont(path))
+    return w
