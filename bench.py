@@ -41,11 +41,25 @@ def cpu_model():
     return "unknown"
 
 
+WORKLOADS = {  # BASELINE.json configs[1..4]: default width, spp
+    "c2": (1920, 512),
+    "c3": (800, 1024),
+    "c4": (1920, 256),
+    "c5": (3840, 4096),
+}
+
+
 def build_workload(scenes, scene, workload, width, spp):
     """(world, lights, cam, description) of a bench workload."""
     if workload == "c2":
         world, lights, cam = scenes.random_spheres(scene, width, spp)
         return world, lights, cam, "C2: book-1 random spheres"
+    if workload == "c3":
+        world, lights, cam = scenes.cornell_smoke(scene, width, spp)
+        return world, lights, cam, "C3: book-2 Cornell box + smoke boxes (quads, media, light sampling)"
+    if workload == "c5":
+        world, lights, cam = scenes.final_scene(scene, width, spp, 40, aspect_ratio=16 / 9)
+        return world, lights, cam, "C5: book-2 final scene, aspect 16/9"
     import tempfile
     obj = os.path.join(tempfile.gettempdir(), "rt_terrain_707", "terrain.obj")
     if not os.path.exists(obj):
@@ -67,7 +81,7 @@ def cpu_baseline(threads, row_stride, spp, workload="c2"):
     scenes = importlib.import_module(PKG + ".scenes")
     api = capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
     scene = rt.Scene(api)
-    world, lights, cam, desc = build_workload(scenes, scene, workload, 1920, spp)
+    world, lights, cam, desc = build_workload(scenes, scene, workload, WORKLOADS[workload][0], spp)
     c = cam.to_c()
     opts = capi.RtRenderOpts()
     api.render_opts_default(ctypes.byref(opts))
@@ -77,14 +91,15 @@ def cpu_baseline(threads, row_stride, spp, workload="c2"):
     opts.threads = threads
     st = capi.RtStats()
     t0 = time.perf_counter()
-    api.check(api.render_f64(scene.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts), None, None, ctypes.byref(st), None))
+    api.check(api.render_f64(scene.s, world.h, -1 if lights is None else lights.h, ctypes.byref(c), ctypes.byref(opts),
+                             None, None, ctypes.byref(st), None))
     dt = time.perf_counter() - t0
     return {
         "value": st.samples / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{desc.split(':')[0]} scene, every {row_stride}th row of 1920x1080 at {spp} spp ({cam.sqrt_spp**2} traced), "
+        "sample": f"{desc.split(':')[0]} scene, every {row_stride}th row of {cam.image_width}x{cam.image_height} at {spp} spp ({cam.sqrt_spp**2} traced), "
                   f"{st.samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
                   "(oracle/: reference-semantics C++ restatement, not the Rust binary)",
     }
@@ -106,10 +121,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2",
-                    help="c2 = BASELINE configs[1] (the headline metric); c4 = configs[3]")
-    ap.add_argument("--spp", type=int, default=None, help="default: 512 (c2), 256 (c4)")
+    ap.add_argument("--width", type=int, default=None, help="default: the config's width")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2",
+                    help="c2 = BASELINE configs[1] (the headline metric); c3 / c4 / c5 = configs[2] / [3] / [4]")
+    ap.add_argument("--spp", type=int, default=None, help="default: the config's spp")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reference-bvh", action="store_true",
@@ -120,7 +135,9 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=None, help="default: 64 (c2), 36 (c4) -> ~10 s of oracle work")
     args = ap.parse_args()
     if args.spp is None:
-        args.spp = 512 if args.workload == "c2" else 256
+        args.spp = WORKLOADS[args.workload][1]
+    if args.width is None:
+        args.width = WORKLOADS[args.workload][0]
 
     import torch
     import torch.distributed as dist
@@ -218,9 +235,10 @@ def main():
         traffic = (load_pmc_traffic(os.path.join(ROOT, "profiles", "r01", f"pmc_{args.workload}.json"))
                    if world_size == 1 else None)
         line = {
-            "metric": ("Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)"
-                       if args.workload == "c2" else
-                       "Msamples/s (pixels x traced spp / s), synthetic 1M-triangle OBJ 1920x1080, 256 spp"),
+            "metric": {"c2": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
+                       "c3": "Msamples/s (pixels x traced spp / s), book-2 Cornell box + smoke 800x800, 1024 spp",
+                       "c4": "Msamples/s (pixels x traced spp / s), synthetic 1M-triangle OBJ 1920x1080, 256 spp",
+                       "c5": "Msamples/s (pixels x traced spp / s), book-2 final scene 3840x2160, 4096 spp"}[args.workload],
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world_size,
@@ -231,9 +249,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("synthetic: book-1 random spheres from SplitMix64(2025) (raytracer-2025_amd/data)"
-                     if args.workload == "c2" else
-                     "synthetic: displaced-grid terrain OBJ/MTL written by scenes.write_terrain_obj(707)")
+            "data": {"c2": "synthetic: book-1 random spheres from SplitMix64(2025) (raytracer-2025_amd/data)",
+                     "c3": "the reference's cornell_box (main.rs:541-639) + two smoke boxes",
+                     "c4": "synthetic: displaced-grid terrain OBJ/MTL written by scenes.write_terrain_obj(707)",
+                     "c5": "the reference's final_scene (main.rs:384-539), randomness from SplitMix64(2025)"}[args.workload]
                     + ", render RNG seed " + str(args.seed),
             "config": {
                 "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth 50, "
@@ -257,7 +276,7 @@ def main():
             },
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            cpu_spp = args.cpu_spp or (64 if args.workload == "c2" else 36)
+            cpu_spp = args.cpu_spp or {"c2": 64, "c3": 64, "c4": 36, "c5": 16}[args.workload]
             line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, cpu_spp, args.workload)
         print(json.dumps(line), flush=True)
     if distributed:

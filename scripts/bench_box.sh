@@ -20,7 +20,8 @@ run() {  # name timeout cmd...
 }
 run bench_c2 400 python3 bench.py
 run bench_c4 600 python3 bench.py --workload c4 --steps 2 --warmup 1
-for w in c2 c4; do
+run bench_c3 400 python3 bench.py --workload c3 --steps 3 --warmup 1
+for w in ${PROFILE_WORKLOADS:-c2 c4 c3}; do
   B="bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline"
   run trace_$w 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$w -o run -- python3 $B
   run fetch_$w 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_$w -o run -- python3 $B

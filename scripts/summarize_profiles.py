@@ -44,7 +44,7 @@ def main(rnd="r01", src="gpurun_out/box"):
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
     summary = {}
-    for w in ("c2", "c4"):
+    for w in ("c2", "c3", "c4", "c5"):
         entry = {}
         ks = os.path.join(src, "trace_" + w, "run_kernel_stats.csv")
         if os.path.exists(ks):

@@ -42,6 +42,10 @@ WEIGHTS = {
     "sky_miss": 17 + 6,        # + environment uv (environment.rs computes it for every miss)
     "medium_tests": 12,
     "light_pdf": 20,
+    # not in the SURVEY table (C3/C5 only): two quaternion rotations (2 x 2 x 15) per instance
+    # entry, and SpherePDF sampling for Isotropic (random_unit_vector + value)
+    "transform_tests": 60,
+    "isotropic": 40,
 }
 BYTES = {"bvh_node_tests": 64, "sphere_tests": 36, "quad_tests": 132, "tri_tests": 132}
 
@@ -56,6 +60,14 @@ def main(workload="c2", row_stride=None, spp=None, threads=0):
         row_stride, spp = row_stride or 8, spp or 16
         world, lights, cam = scenes.random_spheres(scene, 1920, spp)
         desc = "C2 book-1 random spheres 1920x1080, max_depth 50 (per traced sample)"
+    elif workload == "c3":
+        row_stride, spp = row_stride or 4, spp or 16
+        world, lights, cam = scenes.cornell_smoke(scene, 800, spp)
+        desc = "C3 book-2 Cornell box + smoke 800x800, max_depth 10 (per traced sample)"
+    elif workload == "c5":
+        row_stride, spp = row_stride or 16, spp or 4
+        world, lights, cam = scenes.final_scene(scene, 3840, spp, 40, aspect_ratio=16 / 9)
+        desc = "C5 book-2 final scene 3840x2160, max_depth 40 (per traced sample)"
     else:
         import tempfile
         row_stride, spp = row_stride or 16, spp or 4
@@ -73,7 +85,7 @@ def main(workload="c2", row_stride=None, spp=None, threads=0):
     assert n == len(FIELDS)
     counts = (ctypes.c_uint64 * n)()
     st = capi.RtStats()
-    api.check(api.render_f64(scene.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts), None, None, ctypes.byref(st), counts))
+    api.check(api.render_f64(scene.s, world.h, -1 if lights is None else lights.h, ctypes.byref(c), ctypes.byref(opts), None, None, ctypes.byref(st), counts))
     samples = st.samples
     per = {f: counts[i] / samples for i, f in enumerate(FIELDS)}
     flops = sum(per[k] * w for k, w in WEIGHTS.items())

@@ -103,3 +103,10 @@ def test_render_without_gpu_fails_loudly(product, rt, scenes, capi):
     with pytest.raises(capi.RtError) as e:
         cam.render(world, lights)
     assert e.value.code == -7  # RT_EDEVICE, never a silent CPU fallback
+
+
+def test_integration_binds_every_symbol():
+    """INTEGRATION.md's Rust extern block declares every entry point of the header."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    missing = [s for s in declared_symbols() if "fn " + s + "(" not in text]
+    assert not missing, missing
