@@ -276,7 +276,7 @@ def main():
             },
         }
         if world_size == 1 and not args.no_cpu_baseline:
-            cpu_spp = args.cpu_spp or {"c2": 64, "c3": 64, "c4": 36, "c5": 16}[args.workload]
+            cpu_spp = args.cpu_spp or {"c2": 64, "c3": 400, "c4": 36, "c5": 16}[args.workload]
             line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, cpu_spp, args.workload)
         print(json.dumps(line), flush=True)
     if distributed:
