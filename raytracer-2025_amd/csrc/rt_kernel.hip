@@ -232,6 +232,32 @@ __device__ __forceinline__ bool sphere_t(D3 c, double radius, const Ray& r, doub
     return true;
 }
 
+// num / a for a ray's a = |d|^2 with the correctly rounded inva = 1/a computed
+// once per ray: q = num*inva is within 1 ulp, the FMA residual is exact, and
+// the corrected quotient is the correctly rounded num / a (Markstein) -- the
+// value sphere.rs:88-92's division gives, for 3 instructions instead of 10.
+__device__ __forceinline__ double div_a(double num, double a, double inva) {
+    const double q = num * inva;
+    const double r = fma(-q, a, num);
+    return fma(r, inva, q);
+}
+__device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, double a, double inva, double tmin,
+                                             double tmax, double& t) {
+    const D3 oc = c - r.o;
+    const double h = dot(r.d, oc);
+    const double cc = len2(oc) - radius * radius;
+    const double disc = h * h - a * cc;
+    if (disc < 0.0) return false;
+    const double sq = sqrt(disc);
+    double root = div_a(h - sq, a, inva);
+    if (!(root >= tmin && root <= tmax)) {
+        root = div_a(h + sq, a, inva);
+        if (!(root >= tmin && root <= tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
 // quad.rs:71-102 / triangle.rs:69-98
 __device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& r, double tmin, double tmax,
                                          double& t) {
@@ -341,8 +367,8 @@ struct Closest {
 // pushed with its entry distance.
 template <class Stack, class OnHit>
 __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
-                                               double a, double tmin, float tmin_f, Closest& cl, Stack& stk,
-                                               uint32_t& sp, OnHit&& on_hit) {
+                                               double a, double inva, double tmin, float tmin_f, Closest& cl,
+                                               Stack& stk, uint32_t& sp, OnHit&& on_hit) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
     const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
     const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
@@ -361,7 +387,7 @@ __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx,
             const double cz = __hiloint2double(__float_as_int(qb.y), __float_as_int(qb.x));
             const double rr = __hiloint2double(__float_as_int(qb.w), __float_as_int(qb.z));
             double t;
-            if (sphere_t(d3(cx, cy, cz), rr, r, a, tmin, cl.c, t)) {
+            if (sphere_t_inv(d3(cx, cy, cz), rr, r, a, inva, tmin, cl.c, t)) {
                 cl.set(t);
                 on_hit(ch, t);
             }
@@ -400,7 +426,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                            uint32_t sp0, double& tbest) {
     Ray r = r0;
     RayF rf = make_rayf(r);
-    double a = len2(r.d);
+    double a = len2(r.d), inva = 1.0 / a;
     XfIds xfs;
     uint32_t nxf = 0;
     uint32_t sp = sp0;
@@ -419,7 +445,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
         cur = REF_NONE;
         double t;
         switch (kind) {
-            case K_BVH: cur = visit_node(S, idx, r, rf, a, tmin, tmin_f, cl, stk, sp, on_hit); break;
+            case K_BVH: cur = visit_node(S, idx, r, rf, a, inva, tmin, tmin_f, cl, stk, sp, on_hit); break;
             case K_LIST: {
                 const uint32_t child = S.list_children[idx];
                 if (child != REF_NONE) {
@@ -430,7 +456,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             }
             case K_SPHERE: {
                 const double4 s = S.spheres[idx];
-                if (sphere_t(d3(s.x, s.y, s.z), s.w, r, a, tmin, cl.c, t)) {
+                if (sphere_t_inv(d3(s.x, s.y, s.z), s.w, r, a, inva, tmin, cl.c, t)) {
                     cl.set(t);
                     found = true;
                 }
@@ -439,7 +465,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             case K_MSPHERE: {
                 const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
                 const D3 cc = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-                if (sphere_t(cc, s.w, r, a, tmin, cl.c, t)) {
+                if (sphere_t_inv(cc, s.w, r, a, inva, tmin, cl.c, t)) {
                     cl.set(t);
                     found = true;
                 }
@@ -459,6 +485,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 r = xf_ray(X, r);
                 rf = make_rayf(r);
                 a = len2(r.d);
+                inva = 1.0 / a;
                 cur = X.child;
                 break;
             }
@@ -468,6 +495,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 for (uint32_t k = 0; k < nxf; ++k) r = xf_ray(S.xforms[xfs.get(k)], r);
                 rf = make_rayf(r);
                 a = len2(r.d);
+                inva = 1.0 / a;
                 break;
             }
             default: break;
@@ -489,7 +517,7 @@ template <int TIER>
 struct Trav {
     Ray r;  // the ray in the frame of the innermost Transform entered (FULL only)
     RayF rf;
-    double a;
+    double a, inva;  // |d|^2 and its correctly rounded reciprocal
     Closest cl;
     uint32_t cur, sp, nxf;
     XfIds xfs;
@@ -502,6 +530,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     T.r = wr;
     T.rf = make_rayf(wr);
     T.a = len2(wr.d);
+    T.inva = 1.0 / T.a;
     T.cl.c = __builtin_huge_val();
     T.cl.c_f = __builtin_huge_valf();
     T.cur = S.world_root;
@@ -547,10 +576,10 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
     if (kind == K_BVH) {
-        T.cur = visit_node(S, idx, r, T.rf, T.a, tmin, tmin_f, T.cl, stk, T.sp, record);
+        T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
     } else if (kind == K_SPHERE) {
         const double4 sp4 = S.spheres[idx];
-        got = sphere_t(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, tmin, T.cl.c, t);
+        got = sphere_t_inv(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, T.inva, tmin, T.cl.c, t);
     } else if (kind == K_LIST) {
         const uint32_t child = S.list_children[idx];
         if (child != REF_NONE) {
@@ -564,7 +593,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
             case K_MSPHERE: {
                 const double4 s4 = S.msph_center[idx], m = S.msph_dir[idx];
                 const D3 cc = d3(s4.x, s4.y, s4.z) + r.time * d3(m.x, m.y, m.z);
-                got = sphere_t(cc, s4.w, r, T.a, tmin, T.cl.c, t);
+                got = sphere_t_inv(cc, s4.w, r, T.a, T.inva, tmin, T.cl.c, t);
                 break;
             }
             case K_QUAD:
@@ -576,6 +605,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 T.r = xf_ray(X, T.r);
                 T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
+                T.inva = 1.0 / T.a;
                 T.cur = X.child;
                 break;
             }
@@ -585,6 +615,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 for (uint32_t k = 0; k < T.nxf; ++k) T.r = xf_ray(S.xforms[T.xfs.get(k)], T.r);
                 T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
+                T.inva = 1.0 / T.a;
                 break;
             }
             case K_MEDIUM: {
@@ -614,6 +645,132 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         record(this_ref, t);
     }
     return true;
+}
+
+// ------------------------------------------------------------------ basic tier: deferred sphere tests
+// The basic tier's nodes hold two f32 boxes (every sphere child's slot is the
+// sphere's box, rtk_nodes_boxes_only).  A node visit is then the same f32 work
+// on every lane; a sphere whose box is hit is not tested there but queued in
+// the lane's pending list, and the wave runs sphere rounds (every lane with a
+// pending sphere tests one, f64) only when enough lanes have one queued or no
+// lane can walk further.  Node rounds and sphere rounds never share a branch,
+// so the wave pays for each f64 sphere test once per round, not once per node
+// visit that had a sphere child on any lane (the union of both paths).
+#ifndef RT_DEFER_BASIC
+#define RT_DEFER_BASIC 0  // A/B: 0.9-14 % slower than the inline sphere tests
+#endif
+#ifndef RT_DEFER_THRESH
+#define RT_DEFER_THRESH 32  // lanes with a queued sphere that trigger a sphere round
+#endif
+#ifndef RT_DEFER_BLOCKED
+#define RT_DEFER_BLOCKED 65  // lanes blocked on a full pending list that trigger one (65 = never)
+#endif
+
+// Up to 4 queued sphere indices, oldest first, in named registers.
+struct Pending {
+    uint32_t n = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    // selects, not branches: a branch chain is re-formed into an indexed
+    // private array, which the compiler places in scratch memory
+    __device__ __forceinline__ void push(uint32_t v) {
+        q0 = n == 0 ? v : q0;
+        q1 = n == 1 ? v : q1;
+        q2 = n == 2 ? v : q2;
+        q3 = n == 3 ? v : q3;
+        ++n;
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t v = q0;
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+        --n;
+        return v;
+    }
+};
+
+// One box-only node: both slabs in f32; hit sphere children go to the pending
+// list (nearer first), hit inner children are walked near-first.
+template <class Stack>
+__device__ __forceinline__ uint32_t visit_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
+                                                float c_f, Stack& stk, uint32_t& sp, Pending& pd) {
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
+    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
+    const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
+    float e0, e1;
+    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
+    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
+    const bool h0 = slab_f(lo0, hi0, rf, tmin_f, c_f, e0) && c0 != REF_NONE;
+    const bool h1 = slab_f(lo1, hi1, rf, tmin_f, c_f, e1) && c1 != REF_NONE;
+    const bool s0 = h0 && ref_kind(c0) == K_SPHERE, s1 = h1 && ref_kind(c1) == K_SPHERE;
+    if (s0 && s1) {
+        const bool first0 = e0 <= e1;
+        pd.push(ref_index(first0 ? c0 : c1));
+        pd.push(ref_index(first0 ? c1 : c0));
+    } else if (s0) {
+        pd.push(ref_index(c0));
+    } else if (s1) {
+        pd.push(ref_index(c1));
+    }
+    const bool w0 = h0 && !s0, w1 = h1 && !s1;
+    if (w0 && w1) {
+        const bool first0 = e0 <= e1;
+        stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
+        return first0 ? c0 : c1;
+    }
+    return w0 ? c0 : (w1 ? c1 : REF_NONE);
+}
+
+// world.hit for the basic tier (spheres, lists, BVHs): node rounds and sphere
+// rounds, as above.  Same closest hit as trace_step's walk.
+template <class Stack>
+__device__ __forceinline__ void trace_basic(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
+                                            Diag& dg) {
+    constexpr double tmin = 1e-8;
+    const float tmin_f = f32_down(tmin);
+    const double inva = T.inva;
+    Pending pd;
+    for (;;) {
+        const bool has_walk = T.cur != REF_NONE || T.sp > 0;
+        const bool can_walk = has_walk && pd.n <= 2;
+        const unsigned long long mw = __ballot(can_walk);
+        const unsigned long long mp = __ballot(pd.n > 0);
+        if ((mw | mp) == 0) break;
+        RT_DIAG_ONLY(++dg.wave_trace_iters;)
+        // lanes that still have walking to do but a full pending list
+        const unsigned long long mb = __ballot(has_walk && !can_walk);
+        if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH || __popcll(mb) >= RT_DEFER_BLOCKED) {
+            if (pd.n > 0) {  // sphere round (sphere.rs:77-108)
+                RT_DIAG_ONLY(++dg.lane_trace_iters; ++dg.sphere_tests;)
+                const uint32_t idx = pd.pop();
+                const double4 s4 = S.spheres[idx];
+                double t;
+                if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, inva, tmin, T.cl.c, t)) {
+                    T.cl.set(t);
+                    T.found = true;
+                    T.hit.t = t;
+                    T.hit.ref = make_ref(K_SPHERE, idx);
+                }
+            }
+        } else if (can_walk) {  // node round
+            RT_DIAG_ONLY(++dg.lane_trace_iters;)
+            if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+            const uint32_t cur = T.cur;
+            T.cur = REF_NONE;
+            const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+            if (kind == K_BVH) {
+                RT_DIAG_ONLY(++dg.node_visits;)
+                T.cur = visit_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp, pd);
+            } else if (kind == K_LIST) {
+                const uint32_t child = S.list_children[idx];
+                if (child != REF_NONE) {
+                    if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+                    T.cur = child;
+                }
+            } else if (kind == K_SPHERE) {
+                pd.push(idx);
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------ hit record
@@ -994,6 +1151,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #ifndef RT_SHADE_BATCH_FULL
 #define RT_SHADE_BATCH_FULL 64
 #endif
+#ifndef RT_QUEUE_CHUNK
+#define RT_QUEUE_CHUNK 256  // items a wave takes per queue atomic (>= 64)
+#endif
 #ifndef RT_MESH_WAVES
 #define RT_MESH_WAVES 4  // 4-wave budget (some spills) beats 2 waves: 164.7 vs 263.8 ms (C4, 64 spp)
 #endif
@@ -1033,22 +1193,37 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
     uint32_t vertex = 0;
     uint32_t n_rays = 0, n_panics = 0;
 
+    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: items this wave holds
     Diag dg;
     Trav<TIER> T;
     bool walking = false;
     for (;;) {
         RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
-        // ---- refill: wave-aggregated dequeue of stratum rows
+        // ---- refill: wave-aggregated dequeue of stratum rows.  The wave takes
+        // RT_QUEUE_CHUNK items per atomic into a wave-uniform pool and hands them
+        // to its lanes in rank order: one contended atomic per chunk, not one per
+        // main-loop iteration (every iteration some lane of the wave needs work).
         const unsigned long long mask = __ballot(need);
         if (mask) {
-            const uint32_t leader = __ffsll((long long)mask) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(queue, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
+            const uint32_t n = (uint32_t)__popcll(mask);
+            const uint32_t avail = pool_end - pool_next;
+            uint32_t fresh = 0;
+            if (avail < n) {
+                const uint32_t leader = __ffsll((long long)mask) - 1;
+                if (lane == leader) fresh = atomicAdd(queue, (uint32_t)RT_QUEUE_CHUNK);
+                fresh = __shfl(fresh, leader);
+            }
+            const uint32_t old_next = pool_next;
+            if (avail < n) {
+                pool_next = fresh + (n - avail);
+                pool_end = fresh + RT_QUEUE_CHUNK;
+            } else {
+                pool_next += n;
+            }
             if (need) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                item = base + rank;
+                item = rank < avail ? old_next + rank : fresh + (rank - avail);
                 if (item >= F.total_items) break;
                 need = false;
                 s_j = 0;
@@ -1100,7 +1275,10 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
                             : (TIER == TIER_MESH ? RT_SHADE_BATCH_MESH : RT_SHADE_BATCH_FULL);
-        if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
+        if constexpr (TIER == TIER_BASIC && RT_DEFER_BASIC) {
+            trace_basic(S, ray, T, stk, dg);
+            walking = false;
+        } else if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
             while (walking) {
                 RT_DIAG_ONLY(++dg.wave_trace_iters;)
                 walking = trace_step<TIER>(S, ray, T, stk, rng, dg);
@@ -1253,6 +1431,8 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;
 }
+
+extern "C" int rtk_nodes_boxes_only(int tier) { return tier == rtk::TIER_BASIC && RT_DEFER_BASIC; }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
     return tier == rtk::TIER_BASIC ? RT_STACK_BASIC : RT_STACK_MAX;

@@ -113,6 +113,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     if (rc != RT_OK) return rc;
     const int tier = rtk_tier_for(hw.features, hw.stack_need);
+    if (rtk_nodes_boxes_only(tier)) nodes_boxes_only(hw);
     const uint32_t stack_cap = rtk_stack_entries(tier);
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +

@@ -1051,3 +1051,22 @@ void rt_scene_destroy(rt_scene* s) {
 }
 
 }  // extern "C"
+
+namespace rth {
+void nodes_boxes_only(HostWorld& hw) {
+    for (rtk::DNode& n : hw.nodes) {
+        const uint32_t refs[2] = {n.c0, n.c1};
+        for (int k = 0; k < 2; ++k) {
+            if (rtk::ref_kind(refs[k]) != rtk::K_SPHERE) continue;
+            const double c[3] = {n.slot[k].sphere[0], n.slot[k].sphere[1], n.slot[k].sphere[2]};
+            const double r = n.slot[k].sphere[3];
+            auto& bx = n.slot[k].box;
+            for (int a = 0; a < 3; ++a) {
+                bx.lo[a] = round_down(c[a] - r);
+                bx.hi[a] = round_up(c[a] + r);
+            }
+            bx.pad[0] = bx.pad[1] = 0;
+        }
+    }
+}
+}  // namespace rth

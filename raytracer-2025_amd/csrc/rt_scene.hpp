@@ -154,5 +154,9 @@ int32_t set_error(int32_t code, const std::string& msg);
 // the binned-SAH rebuild (closest-hit results agree up to exact t ties).
 int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, bool reference_bvh,
                 HostWorld& out);
+// Rewrites every sphere child slot of every BVH node as the sphere's f32 box
+// (rounded outward): the node format of kernel tiers that queue sphere tests
+// instead of running them inside the node visit (rtk_nodes_boxes_only).
+void nodes_boxes_only(HostWorld& hw);
 void destroy_device_world(DeviceWorld* d);
 }  // namespace rth
