@@ -185,14 +185,6 @@ __device__ __forceinline__ RayF make_rayf(const Ray& r) {
     }
     return R;
 }
-__device__ __forceinline__ float f32_up(double x) {
-    float f = (float)x;
-    if ((double)f < x) {
-        const uint32_t b = __float_as_uint(f);
-        f = (f > 0.0f) ? __uint_as_float(b + 1u) : (f == 0.0f ? 1.401298464e-45f : __uint_as_float(b - 1u));
-    }
-    return f;
-}
 __device__ __forceinline__ bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f,
                                        float& entry) {
     const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
@@ -355,9 +347,13 @@ __device__ __forceinline__ float f32_down(double x) {
 struct Closest {
     double c;
     float c_f;
+    // c_f = (float)t plus at least one ulp: an upper bound of t in two
+    // instructions (|f| * 2^-23 >= 1 ulp of f, and (float)t is within half an
+    // ulp), where the exact round-up takes a compare-and-step sequence.
     __device__ __forceinline__ void set(double t) {
         c = t;
-        c_f = f32_up(t);
+        const float f = (float)t;
+        c_f = fmaf(fabsf(f), 1.1920928955078125e-07f, f);
     }
 };
 
@@ -963,6 +959,10 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
 
+#ifndef RT_HOIST_DRAWS
+#define RT_HOIST_DRAWS 1
+#endif
+
 // ------------------------------------------------------------------ one ray_color level
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
@@ -991,6 +991,17 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     const Rec rec = make_record<TIER>(S, ray, h, panic);
     if (panic) return true;
     DMaterial M = S.materials[rec.mat];
+    // Basic / mesh tiers: every scattering material draws slot 0 (and 1) of
+    // this vertex first, and Lambertian and Metal both turn the first draw
+    // into cos/sin(2 pi r1) (vec3.rs:313-322, 333-343).  Drawn once here for
+    // the whole wave instead of once per material branch a lane takes.
+    constexpr bool HOIST = !FULL && RT_HOIST_DRAWS;
+    double xi0 = 0.0, xi1 = 0.0, sn0 = 0.0, cs0 = 0.0;
+    if constexpr (HOIST) {
+        xi0 = rng.next(ovf);
+        xi1 = rng.next(ovf);
+        sincos(2.0 * PI * xi0, &sn0, &cs0);
+    }
     if constexpr (FULL) {
         // emitted (material.rs:30-33, 171-178, 262-266)
         if (M.flags & MF_EMISSIVE) {
@@ -1034,7 +1045,13 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             if (!ok1) return true;
             const D3 rr = unit(reflect(ud, n), ok2);
             if (!ok2) return true;
-            const D3 ruv = random_unit_vector(rng, ovf);
+            D3 ruv;
+            if constexpr (!HOIST) {
+                ruv = random_unit_vector(rng, ovf);
+            } else {
+                const double s = sqrt(xi1 * (1.0 - xi1));
+                ruv = d3(cs0 * 2.0 * s, sn0 * 2.0 * s, 1.0 - 2.0 * xi1);
+            }
             beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
             ray = Ray{rec.p, rr + (M.fuzz * ruv), ray.time};
             break;
@@ -1052,7 +1069,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 const double r0sq = r0 * r0;
                 const double x = 1.0 - cos_theta;
                 const double x2 = x * x;
-                do_reflect = r0sq + (1.0 - r0sq) * (x * (x2 * x2)) > rng.next(ovf);
+                do_reflect = r0sq + (1.0 - r0sq) * (x * (x2 * x2)) > (HOIST ? xi0 : rng.next(ovf));
             }
             D3 dir;
             if (do_reflect) {
@@ -1090,9 +1107,12 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
         bool ok = true;
         if (from_material) {
             if (!FULL || pdf_kind == 0) {  // CosinePDF::generate (pdf.rs:59-63), vec3.rs:333-343
-                const double r1 = rng.next(ovf), r2 = rng.next(ovf);
-                double sn, cs;
-                sincos(2.0 * PI * r1, &sn, &cs);
+                double r2 = xi1, sn = sn0, cs = cs0;
+                if constexpr (!HOIST) {
+                    const double r1 = rng.next(ovf);
+                    r2 = rng.next(ovf);
+                    sincos(2.0 * PI * r1, &sn, &cs);
+                }
                 const double sr2 = sqrt(r2);
                 dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
             } else {

@@ -52,10 +52,11 @@ __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32
             k0 += 0x9E3779B9u;
             k1 += 0xBB67AE85u;
         }
-        const uint32_t lo0 = 0xD2511F53u * c0;
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2);
+        // one v_mad_u64_u32 per 32x32->64 product (not a mul_lo + mul_hi pair)
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         const uint32_t n0 = hi1 ^ c1 ^ k0;
         const uint32_t n2 = hi0 ^ c3 ^ k1;
         c0 = n0;

@@ -30,6 +30,10 @@ if wl == "c4":
     if not os.path.exists(obj):
         scenes.write_terrain_obj(os.path.dirname(obj), 707)
     world, lights, cam = scenes.obj_terrain(scene, obj, 1920, spp)
+elif wl == "c3":
+    world, lights, cam = scenes.cornell_smoke(scene, 800, spp)
+elif wl == "c5":
+    world, lights, cam = scenes.final_scene(scene, 1920, spp, 40, aspect_ratio=16 / 9)
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
