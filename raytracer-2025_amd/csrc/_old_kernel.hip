@@ -501,38 +501,6 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
     return found;
 }
 
-// ConstantMedium::hit (volume.rs:37-73) of medium idx for ray r in the
-// medium's frame, interval [tmin, tmax]: the two boundary hits are one
-// boundary walk run twice (one copy of the walk in the code).
-template <class Stack>
-__device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, const Ray& r, double tmin, double tmax,
-                                           Stack& stk, uint32_t sp0, const Rng& rng, double& t) {
-    const DMedium M = S.media[idx];
-    const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
-    double t1 = 0.0, t2 = 0.0, lo = NINF;
-#pragma nounroll
-    for (int pass = 0; pass < 2; ++pass) {
-        double tb;
-        if (!boundary_t(S, M.boundary, r, lo, PINF, stk, sp0, tb)) return false;
-        if (pass == 0) {
-            t1 = tb;
-            lo = fmin(t1 + 0.0001, PINF);
-        } else {
-            t2 = tb;
-        }
-    }
-    if (t1 < tmin) t1 = tmin;
-    if (t2 > tmax) t2 = tmax;
-    if (t1 >= t2) return false;
-    if (t1 < 0.0) t1 = 0.0;
-    const double ray_length = len(r.d);
-    const double inside = (t2 - t1) * ray_length;
-    const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
-    if (hd > inside) return false;
-    t = t1 + hd / ray_length;  // volume.rs:65
-    return t <= tmax;
-}
-
 // world.hit(r, [1e-8, inf)) (camera.rs:286) as a depth-first walk with one
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
@@ -551,7 +519,6 @@ struct Trav {
     XfIds xfs;
     bool found;
     HitInfo hit;
-    uint32_t nmed;  // FULL: media met by the walk, tested after it (media_phase)
 };
 
 template <int TIER>
@@ -567,13 +534,12 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     T.nxf = 0;
     T.found = false;
     T.hit.nxf = 0;
-    T.nmed = 0;
 }
 
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
 template <int TIER>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                           const Rng& rng, uint4* med, Diag& dg) {
+                                           const Rng& rng, Diag& dg) {
     constexpr bool FULL = TIER == TIER_FULL;
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
@@ -649,17 +615,22 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 break;
             }
             case K_MEDIUM: {
-                // volume.rs:37-73.  The medium's hit is independent of the
-                // other objects but for the interval's upper end, so it is
-                // queued (with the Transforms around it) and tested after the
-                // walk against the walk's closest t (media_phase); only a
-                // lane whose queue is full tests it here.
-                if (T.nmed < RT_MEDIA_CAP) {
-                    med[T.nmed * RT_BLOCK] = make_uint4(idx, T.nxf, T.xfs.a, T.xfs.b);
-                    ++T.nmed;
-                } else {
-                    got = medium_hit(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
-                }
+                // volume.rs:37-73
+                const DMedium M = S.media[idx];
+                double t1, t2;
+                const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
+                if (!boundary_t(S, M.boundary, r, NINF, PINF, stk, T.sp, t1)) break;
+                if (!boundary_t(S, M.boundary, r, fmin(t1 + 0.0001, PINF), PINF, stk, T.sp, t2)) break;
+                if (t1 < tmin) t1 = tmin;
+                if (t2 > T.cl.c) t2 = T.cl.c;
+                if (t1 >= t2) break;
+                if (t1 < 0.0) t1 = 0.0;
+                const double ray_length = len(r.d);
+                const double inside = (t2 - t1) * ray_length;
+                const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
+                if (hd > inside) break;
+                t = t1 + hd / ray_length;  // volume.rs:65
+                got = t <= T.cl.c;
                 break;
             }
             default: break;
@@ -670,29 +641,6 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         record(this_ref, t);
     }
     return true;
-}
-
-// The queued media of a finished walk (FULL tier), each in its own frame,
-// against the walk's closest t; the walk's stack is free again.
-template <int TIER>
-__device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                            const Rng& rng, const uint4* med) {
-    for (uint32_t k = 0; k < T.nmed; ++k) {
-        const uint4 e = med[k * RT_BLOCK];
-        Ray r = wr;
-        for (uint32_t j = 0; j < e.y; ++j) r = xf_ray(S.xforms[j == 0 ? e.z : e.w], r);
-        double t;
-        if (medium_hit(S, e.x, r, 1e-8, T.cl.c, stk, 0, rng, t)) {
-            T.cl.set(t);
-            T.found = true;
-            T.hit.t = t;
-            T.hit.ref = make_ref(K_MEDIUM, e.x);
-            T.hit.nxf = e.y;
-            T.hit.xf.a = e.z;
-            T.hit.xf.b = e.w;
-        }
-    }
-    T.nmed = 0;
 }
 
 // ------------------------------------------------------------------ basic tier: deferred sphere tests
@@ -1250,8 +1198,6 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
     uint32_t* queue = P->queue;
     constexpr int STACK = TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
     __shared__ uint2 stack_lds[STACK * RT_BLOCK];
-    __shared__ uint4 media_lds[TIER == TIER_FULL && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
-    uint4* med = media_lds + threadIdx.x;
     StackFor<TIER> stk{stack_lds + threadIdx.x,
                        P->stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x, gridDim.x * RT_BLOCK};
     const uint32_t lane = __lane_id();
@@ -1355,22 +1301,18 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
         } else if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
             while (walking) {
                 RT_DIAG_ONLY(++dg.wave_trace_iters;)
-                walking = trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                walking = trace_step<TIER>(S, ray, T, stk, rng, dg);
             }
-            if constexpr (TIER == TIER_FULL) media_phase<TIER>(S, ray, T, stk, rng, med);
         } else {
             const unsigned long long active = __ballot(true);
             for (;;) {
                 RT_DIAG_ONLY(++dg.wave_trace_iters;)
-                if (walking) walking = trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                if (walking) walking = trace_step<TIER>(S, ray, T, stk, rng, dg);
                 const unsigned long long w = __ballot(walking);
                 if (w == 0 || __popcll(active & ~w) >= BATCH) break;
             }
         }
         RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
-        if constexpr (BATCH < 64 && TIER == TIER_FULL) {
-            if (!walking) media_phase<TIER>(S, ray, T, stk, rng, med);
-        }
         if (BATCH < 64 && walking) continue;
         bool panic = false;
         bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic);

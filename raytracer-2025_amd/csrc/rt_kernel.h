@@ -12,6 +12,9 @@
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
 #define RT_STACK_MAX 64     // LDS + overflow entries (mesh and full tiers)
+#ifndef RT_MEDIA_CAP
+#define RT_MEDIA_CAP 2      // full tier: media a walk queues (in LDS, 16 B each) before testing them inline
+#endif
 
 namespace rtk {
 // Kernel tiers: the launcher picks the smallest that covers the flattened world.
