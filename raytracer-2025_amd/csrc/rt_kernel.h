@@ -40,8 +40,10 @@ struct rtk_frame_desc {
 
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" uint32_t rtk_stack_entries(int tier);
-// 1 if the tier's kernel expects every BVH child slot as a box (rth::nodes_boxes_only)
-extern "C" int rtk_nodes_boxes_only(int tier);
+// 1 if the tier's kernel expects sphere child slots as f32 filter records (rth::nodes_sphere_f32)
+extern "C" int rtk_node_sphere_f32(int tier);
+// 1 if the basic tier's kernel walks 4-wide BVH nodes (rth::bvh4_basic)
+extern "C" int rtk_basic_bvh4(void);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
                                        int toon, hipStream_t stream, int tier, int grid, void* params_dev,

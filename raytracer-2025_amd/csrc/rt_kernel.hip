@@ -24,6 +24,17 @@
 
 namespace rtk {
 
+// Basic tier: f32 sphere filter + queued exact f64 sphere tests (sphere_filter); 0 = inline f64 tests.
+#ifndef RT_SPHERE_FILTER
+#define RT_SPHERE_FILTER 0
+#endif
+// Basic tier: 4-wide BVH nodes (rth::bvh4_basic), sphere children through the
+// filter into a per-lane LDS queue of exact tests (visit4); implies the filter.
+#ifndef RT_BVH4
+#define RT_BVH4 1
+#endif
+#define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
+
 // Diagnostic build (-DRT_DIAG, librt_mi355x_diag.so only): per-wave cycle
 // stamps and per-lane work counters, summed into g_diag.  The product build
 // compiles all of it away.
@@ -185,6 +196,31 @@ __device__ __forceinline__ RayF make_rayf(const Ray& r) {
     }
     return R;
 }
+// Per-ray f32 data of the basic tier's sphere filter (sphere_filter below).
+struct SphF {
+    float o[3], d[3];
+    float a;    // |d|^2
+    float gr;   // |o|_1 rounded up
+    float ka;   // 2^-17 a: discriminant error bound per G^2
+    float ehd;  // 2^-19 |d|: error bound of h per G
+    float ia;   // 1/a rounded up (with margin)
+};
+__device__ __forceinline__ SphF make_sphf(const Ray& r) {
+    SphF F;
+    F.o[0] = (float)r.o.x;
+    F.o[1] = (float)r.o.y;
+    F.o[2] = (float)r.o.z;
+    F.d[0] = (float)r.d.x;
+    F.d[1] = (float)r.d.y;
+    F.d[2] = (float)r.d.z;
+    F.a = fmaf(F.d[2], F.d[2], fmaf(F.d[1], F.d[1], F.d[0] * F.d[0]));
+    F.gr = (fabsf(F.o[0]) + fabsf(F.o[1]) + fabsf(F.o[2])) * (1.0f + 0x1p-20f);
+    F.ka = F.a * 0x1p-17f;
+    F.ehd = sqrtf(F.a) * 0x1p-19f;
+    F.ia = (1.0f / F.a) * (1.0f + 0x1p-19f);
+    return F;
+}
+
 __device__ __forceinline__ bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f,
                                        float& entry) {
     const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
@@ -355,6 +391,12 @@ struct Closest {
         const float f = (float)t;
         c_f = fmaf(fabsf(f), 1.1920928955078125e-07f, f);
     }
+    // a hit t <= c found while c_f may already be a tighter bound (sphere filter)
+    __device__ __forceinline__ void lower(double t) {
+        c = t;
+        const float f = (float)t;
+        c_f = fminf(c_f, fmaf(fabsf(f), 1.1920928955078125e-07f, f));
+    }
 };
 
 // One BVH node visit (one 80-B record): a sphere child is intersected right
@@ -400,6 +442,66 @@ __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx,
         return first0 ? c0 : c1;
     }
     return h0 ? c0 : (h1 ? c1 : REF_NONE);
+}
+
+#ifndef RT_BRANCHLESS
+#define RT_BRANCHLESS 0
+#endif
+// sphere.rs:77-108 with selects instead of branches: both roots, the first
+// accepted one (same result as sphere_t_inv).
+__device__ __forceinline__ bool sphere_t_sel(D3 c, double radius, const Ray& r, double a, double inva, double tmin,
+                                             double tmax, double& t) {
+    const D3 oc = c - r.o;
+    const double h = dot(r.d, oc);
+    const double cc = len2(oc) - radius * radius;
+    const double disc = h * h - a * cc;
+    const double sq = sqrt(fmax(disc, 0.0));
+    const double r1 = div_a(h - sq, a, inva), r2 = div_a(h + sq, a, inva);
+    const bool ok1 = r1 >= tmin && r1 <= tmax, ok2 = r2 >= tmin && r2 <= tmax;
+    t = ok1 ? r1 : r2;
+    return disc >= 0.0 && (ok1 || ok2);
+}
+
+// visit_node for a wave whose lanes diverge between sphere and box children:
+// every lane computes both children's sphere tests (skipped only when no lane
+// of the wave has a sphere child) and both slab tests, and keeps its results
+// with selects -- the work of the union of the two paths, which the wave pays
+// anyway, without the exec-mask bookkeeping of nested divergent branches.
+template <class Stack>
+__device__ __forceinline__ uint32_t visit_node_sel(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
+                                                   double a, double inva, double tmin, float tmin_f, Closest& cl,
+                                                   bool& found, HitInfo& hit, Stack& stk, uint32_t& sp) {
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
+    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
+    const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
+    const bool s0 = ref_kind(c0) == K_SPHERE, s1 = ref_kind(c1) == K_SPHERE;
+    if (__ballot(s0 || s1)) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t ch = k ? c1 : c0;
+            const float4 qa = k ? q2 : q0, qb = k ? q3 : q1;
+            const double cx = __hiloint2double(__float_as_int(qa.y), __float_as_int(qa.x));
+            const double cy = __hiloint2double(__float_as_int(qa.w), __float_as_int(qa.z));
+            const double cz = __hiloint2double(__float_as_int(qb.y), __float_as_int(qb.x));
+            const double rr = __hiloint2double(__float_as_int(qb.w), __float_as_int(qb.z));
+            double t;
+            const bool h = sphere_t_sel(d3(cx, cy, cz), rr, r, a, inva, tmin, cl.c, t) && (k ? s1 : s0);
+            const float f = (float)t;
+            cl.c = h ? t : cl.c;
+            cl.c_f = h ? fmaf(fabsf(f), 1.1920928955078125e-07f, f) : cl.c_f;
+            found = found || h;
+            hit.t = h ? t : hit.t;
+            hit.ref = h ? ch : hit.ref;
+        }
+    }
+    float e0, e1;
+    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
+    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
+    const bool h0 = slab_f(lo0, hi0, rf, tmin_f, cl.c_f, e0) && c0 != REF_NONE && !s0;
+    const bool h1 = slab_f(lo1, hi1, rf, tmin_f, cl.c_f, e1) && c1 != REF_NONE && !s1;
+    const bool first0 = e0 <= e1;
+    if (h0 && h1) stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
+    return (h0 && (first0 || !h1)) ? c0 : (h1 ? c1 : REF_NONE);
 }
 
 // Pops until an entry whose box can still hold a hit closer than c.
@@ -533,6 +635,57 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
     return t <= tmax;
 }
 
+// sphere_filter for lanes that may hold no sphere (is_sph false): same
+// decisions, taken with selects.
+__device__ __forceinline__ bool sphere_filter_sel(const float4 qa, const float4 qb, const SphF& F, float& c_f,
+                                                  bool is_sph) {
+    const float ocx = qa.x - F.o[0], ocy = qa.y - F.o[1], ocz = qa.z - F.o[2];
+    const float r = qa.w;
+    const float h = fmaf(F.d[2], ocz, fmaf(F.d[1], ocy, F.d[0] * ocx));
+    const float q = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx));
+    const float cc = fmaf(-r, r, q);
+    const float disc = fmaf(h, h, -(F.a * cc));
+    const float G = qb.x + F.gr, G2 = G * G;
+    const float m = F.ka * G2;
+    const float eh = F.ehd * G;
+    const float hh = h + eh;
+    const float clo = fmaf(-0x1p-19f, G2, cc);
+    const bool outside = clo > 0.0f;
+    const bool miss = disc < -m || (outside && (hh < 0.0f || clo > 2.0004f * hh * c_f));
+    const bool sure = outside && disc > m && h > eh && clo > 2.1e-8f * hh;
+    c_f = (is_sph && !miss && sure) ? fminf(c_f, hh * F.ia) : c_f;
+    return is_sph && !miss;
+}
+
+// Up to 4 queued sphere indices, oldest first, in named registers.
+struct Pending {
+    uint32_t n = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+    // selects, not branches: a branch chain is re-formed into an indexed
+    // private array, which the compiler places in scratch memory
+    __device__ __forceinline__ void push(uint32_t v) {
+        q0 = n == 0 ? v : q0;
+        q1 = n == 1 ? v : q1;
+        q2 = n == 2 ? v : q2;
+        q3 = n == 3 ? v : q3;
+        ++n;
+    }
+    __device__ __forceinline__ void push_if(bool c, uint32_t v) {
+        q0 = (c && n == 0) ? v : q0;
+        q1 = (c && n == 1) ? v : q1;
+        q2 = (c && n == 2) ? v : q2;
+        q3 = (c && n == 3) ? v : q3;
+        n += c ? 1u : 0u;
+    }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t v = q0;
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+        --n;
+        return v;
+    }
+};
+
 // world.hit(r, [1e-8, inf)) (camera.rs:286) as a depth-first walk with one
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
@@ -552,6 +705,8 @@ struct Trav {
     bool found;
     HitInfo hit;
     uint32_t nmed;  // FULL: media met by the walk, tested after it (media_phase)
+    SphF sf;        // BASIC with the sphere filter: per-ray f32 data
+    Pending pd;     // and the spheres queued for the exact test
 };
 
 template <int TIER>
@@ -568,6 +723,10 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     T.found = false;
     T.hit.nxf = 0;
     T.nmed = 0;
+    if constexpr (TIER == TIER_BASIC && (RT_SPHERE_FILTER || RT_BVH4)) {
+        T.sf = make_sphf(wr);
+        T.pd.n = 0;
+    }
 }
 
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
@@ -606,7 +765,10 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
     if (kind == K_BVH) {
-        T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
+        if constexpr (TIER == TIER_BASIC && RT_BRANCHLESS)
+            T.cur = visit_node_sel(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, T.found, T.hit, stk, T.sp);
+        else
+            T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
     } else if (kind == K_SPHERE) {
         const double4 sp4 = S.spheres[idx];
         got = sphere_t_inv(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, T.inva, tmin, T.cl.c, t);
@@ -695,130 +857,267 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, T
     T.nmed = 0;
 }
 
-// ------------------------------------------------------------------ basic tier: deferred sphere tests
-// The basic tier's nodes hold two f32 boxes (every sphere child's slot is the
-// sphere's box, rtk_nodes_boxes_only).  A node visit is then the same f32 work
-// on every lane; a sphere whose box is hit is not tested there but queued in
-// the lane's pending list, and the wave runs sphere rounds (every lane with a
-// pending sphere tests one, f64) only when enough lanes have one queued or no
-// lane can walk further.  Node rounds and sphere rounds never share a branch,
-// so the wave pays for each f64 sphere test once per round, not once per node
-// visit that had a sphere child on any lane (the union of both paths).
-#ifndef RT_DEFER_BASIC
-#define RT_DEFER_BASIC 0  // A/B: 0.9-14 % slower than the inline sphere tests
-#endif
+// ------------------------------------------------------------------ basic tier: f32 sphere filter
+// Inline, a node visit runs the f64 sphere test (sphere.rs:77-108) of every
+// sphere child, and a wave pays for the union of the sphere path and the box
+// path of its lanes -- on C2 almost every visit.  With the filter, a sphere
+// child's slot holds the sphere in f32 (rt_layout.h DNodeSlot::fsph) and the
+// visit runs a conservative f32 test:
+//  - it rejects only spheres the exact test is certain to miss: discriminant
+//    below minus its error bound, the sphere behind an origin outside it, or
+//    its near root beyond the walk's f32 bound of the closest t;
+//  - when the near root is certain to be accepted, its upper bound h/a
+//    (closest approach, >= the near root) lowers that bound at once, so the
+//    walk culls as it did with the exact test;
+//  - every other sphere is queued (idx, up to 4 per lane, in registers) and
+//    tested exactly in f64 in sphere rounds, which the wave runs when enough
+//    lanes have one queued or no lane can walk further.
+// Error bounds (u = 2^-24, G = |c|_1 + r + |o|_1 >= every magnitude involved,
+// inputs rounded to nearest f32): |h - h*| <= 6.2u |d| G, |cc - cc*| <= 10.4u G^2,
+// |disc - disc*| <= 31u a G^2; the kernel uses 32u |d| G, 32u G^2 and 128u a G^2.
+// The reference's own f64 rounding is orders of magnitude below these.  So the
+// closest hit is the one the inline f64 tests find (tests/test_parity_gpu.py).
 #ifndef RT_DEFER_THRESH
-#define RT_DEFER_THRESH 32  // lanes with a queued sphere that trigger a sphere round
+#define RT_DEFER_THRESH 48  // lanes with a queued sphere that trigger a sphere round
 #endif
 #ifndef RT_DEFER_BLOCKED
-#define RT_DEFER_BLOCKED 65  // lanes blocked on a full pending list that trigger one (65 = never)
+#define RT_DEFER_BLOCKED 65  // lanes blocked on a full queue that trigger one (65 = never)
 #endif
 
-// Up to 4 queued sphere indices, oldest first, in named registers.
-struct Pending {
-    uint32_t n = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-    // selects, not branches: a branch chain is re-formed into an indexed
-    // private array, which the compiler places in scratch memory
-    __device__ __forceinline__ void push(uint32_t v) {
-        q0 = n == 0 ? v : q0;
-        q1 = n == 1 ? v : q1;
-        q2 = n == 2 ? v : q2;
-        q3 = n == 3 ? v : q3;
-        ++n;
-    }
-    __device__ __forceinline__ uint32_t pop() {
-        const uint32_t v = q0;
-        q0 = q1;
-        q1 = q2;
-        q2 = q3;
-        --n;
-        return v;
-    }
-};
+// The f32 sphere test of one fsph slot {c, r | g}: false when the exact test
+// is certain not to give a hit closer than c_f; lowers c_f when it is certain
+// to give one.
+__device__ __forceinline__ bool sphere_filter(const float4 qa, const float4 qb, const SphF& F, float& c_f) {
+    const float ocx = qa.x - F.o[0], ocy = qa.y - F.o[1], ocz = qa.z - F.o[2];
+    const float r = qa.w;
+    const float h = fmaf(F.d[2], ocz, fmaf(F.d[1], ocy, F.d[0] * ocx));
+    const float q = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx));
+    const float cc = fmaf(-r, r, q);
+    const float disc = fmaf(h, h, -(F.a * cc));
+    const float G = qb.x + F.gr, G2 = G * G;
+    const float m = F.ka * G2;
+    const float eh = F.ehd * G;
+    const float hh = h + eh;                        // >= h
+    const float clo = fmaf(-0x1p-19f, G2, cc);      // <= cc
+    const bool outside = clo > 0.0f;                // origin certainly outside: roots of one sign
+    // near root >= cc / 2h > c_f (both roots beyond the bound), or both roots < 0
+    if (disc < -m || (outside && (hh < 0.0f || clo > 2.0004f * hh * c_f))) return false;
+    // near root certainly >= t_min (cc / 2h > 1e-8) and the ray certainly hits: t <= h / a
+    if (outside && disc > m && h > eh && clo > 2.1e-8f * hh) c_f = fminf(c_f, hh * F.ia);
+    return true;
+}
 
-// One box-only node: both slabs in f32; hit sphere children go to the pending
-// list (nearer first), hit inner children are walked near-first.
+// One node visit with filtered sphere children: box children get the f32
+// slab test and are walked near-first; sphere children the filter (queued).
 template <class Stack>
-__device__ __forceinline__ uint32_t visit_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
-                                                float c_f, Stack& stk, uint32_t& sp, Pending& pd) {
+__device__ __forceinline__ uint32_t visit_filtered(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
+                                                   float tmin_f, float& c_f, Stack& stk, uint32_t& sp, Pending& pd) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
     const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
     const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
-    float e0, e1;
-    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
-    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
-    const bool h0 = slab_f(lo0, hi0, rf, tmin_f, c_f, e0) && c0 != REF_NONE;
-    const bool h1 = slab_f(lo1, hi1, rf, tmin_f, c_f, e1) && c1 != REF_NONE;
-    const bool s0 = h0 && ref_kind(c0) == K_SPHERE, s1 = h1 && ref_kind(c1) == K_SPHERE;
-    if (s0 && s1) {
-        const bool first0 = e0 <= e1;
-        pd.push(ref_index(first0 ? c0 : c1));
-        pd.push(ref_index(first0 ? c1 : c0));
-    } else if (s0) {
-        pd.push(ref_index(c0));
-    } else if (s1) {
-        pd.push(ref_index(c1));
+    bool h0 = false, h1 = false;
+    float e0 = 0.0f, e1 = 0.0f;
+    if constexpr (RT_BRANCHLESS) {  // both filters and both slab tests on every lane, kept by selects
+        const bool s0 = ref_kind(c0) == K_SPHERE, s1 = ref_kind(c1) == K_SPHERE;
+        if (__ballot(s0 || s1)) {
+            const bool k0 = sphere_filter_sel(q0, q1, sf, c_f, s0), k1 = sphere_filter_sel(q2, q3, sf, c_f, s1);
+            pd.push_if(k0, ref_index(c0));
+            pd.push_if(k1, ref_index(c1));
+        }
+        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
+        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
+        h0 = slab_f(lo0, hi0, rf, tmin_f, c_f, e0) && c0 != REF_NONE && !s0;
+        h1 = slab_f(lo1, hi1, rf, tmin_f, c_f, e1) && c1 != REF_NONE && !s1;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t ch = k ? c1 : c0;
+            const float4 qa = k ? q2 : q0, qb = k ? q3 : q1;
+            bool& hk = k ? h1 : h0;
+            float& ek = k ? e1 : e0;
+            if (ch == REF_NONE) continue;
+            if (ref_kind(ch) == K_SPHERE) {
+                if (sphere_filter(qa, qb, sf, c_f)) pd.push(ref_index(ch));
+            } else {
+                const float lo[3] = {qa.x, qa.y, qa.z}, hi[3] = {qa.w, qb.x, qb.y};
+                hk = slab_f(lo, hi, rf, tmin_f, c_f, ek);
+            }
+        }
     }
-    const bool w0 = h0 && !s0, w1 = h1 && !s1;
-    if (w0 && w1) {
+    h0 = h0 && e0 <= c_f;
+    h1 = h1 && e1 <= c_f;
+    if (h0 && h1) {
         const bool first0 = e0 <= e1;
         stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
         return first0 ? c0 : c1;
     }
-    return w0 ? c0 : (w1 ? c1 : REF_NONE);
+    return h0 ? c0 : (h1 ? c1 : REF_NONE);
 }
 
-// world.hit for the basic tier (spheres, lists, BVHs): node rounds and sphere
-// rounds, as above.  Same closest hit as trace_step's walk.
+// world.hit for the basic tier (spheres, lists, BVHs) with the sphere filter,
+// one wave iteration per call: lanes that can walk visit one node (f32 only);
+// then, when enough lanes have a sphere queued (or none walks any more), each
+// of those tests one exactly in f64 (sphere.rs:77-108).  A lane whose queue is
+// full waits for that before walking on.  Returns false when the lane's walk
+// and queue are both done; same closest hit as trace_step's walk.
 template <class Stack>
-__device__ __forceinline__ void trace_basic(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
-                                            Diag& dg) {
+__device__ __forceinline__ bool trace_filtered_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
+                                                    Diag& dg) {
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
-    const double inva = T.inva;
-    Pending pd;
-    for (;;) {
-        const bool has_walk = T.cur != REF_NONE || T.sp > 0;
-        const bool can_walk = has_walk && pd.n <= 2;
-        const unsigned long long mw = __ballot(can_walk);
-        const unsigned long long mp = __ballot(pd.n > 0);
-        if ((mw | mp) == 0) break;
-        RT_DIAG_ONLY(++dg.wave_trace_iters;)
-        // lanes that still have walking to do but a full pending list
-        const unsigned long long mb = __ballot(has_walk && !can_walk);
-        if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH || __popcll(mb) >= RT_DEFER_BLOCKED) {
-            if (pd.n > 0) {  // sphere round (sphere.rs:77-108)
-                RT_DIAG_ONLY(++dg.lane_trace_iters; ++dg.sphere_tests;)
-                const uint32_t idx = pd.pop();
-                const double4 s4 = S.spheres[idx];
-                double t;
-                if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, inva, tmin, T.cl.c, t)) {
-                    T.cl.set(t);
-                    T.found = true;
-                    T.hit.t = t;
-                    T.hit.ref = make_ref(K_SPHERE, idx);
-                }
+    RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
+    if ((T.cur != REF_NONE || T.sp > 0) && T.pd.n <= 2) {  // node round
+        RT_DIAG_ONLY(++dg.lane_trace_iters;)
+        if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+        const uint32_t cur = T.cur;
+        T.cur = REF_NONE;
+        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+        if (kind == K_BVH) {
+            RT_DIAG_ONLY(++dg.node_visits;)
+            T.cur = visit_filtered(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, T.pd);
+        } else if (kind == K_LIST) {
+            const uint32_t child = S.list_children[idx];
+            if (child != REF_NONE) {
+                if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+                T.cur = child;
             }
-        } else if (can_walk) {  // node round
-            RT_DIAG_ONLY(++dg.lane_trace_iters;)
-            if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
-            const uint32_t cur = T.cur;
-            T.cur = REF_NONE;
-            const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
-            if (kind == K_BVH) {
-                RT_DIAG_ONLY(++dg.node_visits;)
-                T.cur = visit_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp, pd);
-            } else if (kind == K_LIST) {
-                const uint32_t child = S.list_children[idx];
-                if (child != REF_NONE) {
-                    if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                    T.cur = child;
-                }
-            } else if (kind == K_SPHERE) {
-                pd.push(idx);
+        } else if (kind == K_SPHERE) {
+            T.pd.push(idx);
+        }
+    }
+    const bool walk = T.cur != REF_NONE || T.sp > 0;
+    // lanes that can walk on without a sphere round: when there are none, the
+    // round runs whatever the count (a lane blocked on a full queue counts as
+    // not walking, else it would wait on itself)
+    const unsigned long long mw = __ballot(walk && T.pd.n <= 2);
+    const unsigned long long mp = __ballot(T.pd.n > 0);
+    const unsigned long long mb = __ballot(walk && T.pd.n > 2);
+    if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH || __popcll(mb) >= RT_DEFER_BLOCKED) {
+        if (T.pd.n > 0) {  // sphere round
+            RT_DIAG_ONLY(++dg.sphere_tests;)
+            const uint32_t idx = T.pd.pop();
+            const double4 s4 = S.spheres[idx];
+            double t;
+            if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
+                T.cl.lower(t);
+                T.found = true;
+                T.hit.t = t;
+                T.hit.ref = make_ref(K_SPHERE, idx);
             }
         }
     }
+    return walk || T.pd.n > 0;
+}
+
+// ------------------------------------------------------------------ basic tier: 4-wide BVH
+// One visit of a DNode4: the sphere children's f32 filter (queued into the
+// lane's LDS queue, pq[k * RT_BLOCK], when the exact test must run), then the
+// four slab tests; the hit boxes are sorted by entry distance, the nearest is
+// walked next and the others pushed farthest first.
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
+                                           float tmin_f, float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq,
+                                           uint32_t& pn) {
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
+    const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], rq = np[6];
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
+    const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
+    bool sph[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sph[i] = ref_kind(R[i]) == K_SPHERE;
+    if (__ballot(sph[0] || sph[1] || sph[2] || sph[3])) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (sphere_filter_sel(make_float4(LX[i], LY[i], LZ[i], HX[i]), make_float4(HY[i], 0.0f, 0.0f, 0.0f), sf,
+                                  c_f, sph[i])) {
+                pq[pn * RT_BLOCK] = ref_index(R[i]);
+                ++pn;
+            }
+        }
+    }
+    constexpr float INF = __builtin_huge_valf();
+    float key[4];
+    uint32_t ref[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float lo[3] = {LX[i], LY[i], LZ[i]}, hi[3] = {HX[i], HY[i], HZ[i]};
+        float e;
+        const bool h = slab_f(lo, hi, rf, tmin_f, c_f, e) && R[i] != REF_NONE && !sph[i];
+        key[i] = h ? e : INF;
+        ref[i] = R[i];
+    }
+    auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
+        const bool sw = key[b] < key[a];
+        const float ka = key[a], kb = key[b];
+        const uint32_t ra = ref[a], rb = ref[b];
+        key[a] = sw ? kb : ka;
+        key[b] = sw ? ka : kb;
+        ref[a] = sw ? rb : ra;
+        ref[b] = sw ? ra : rb;
+    };
+    cs(0, 1);
+    cs(2, 3);
+    cs(0, 2);
+    cs(1, 3);
+    cs(1, 2);
+    if (key[3] < INF) stk.push(sp++, ref[3], key[3]);
+    if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
+    if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
+    return key[0] < INF ? ref[0] : REF_NONE;
+}
+
+// world.hit for the basic tier over 4-wide nodes, one wave iteration per call
+// (as trace_filtered_step): a node round for lanes with room in their queue,
+// then a sphere round when enough lanes have a test queued or none can walk.
+template <class Stack>
+__device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
+                                            uint32_t* pq, Diag& dg) {
+    constexpr double tmin = 1e-8;
+    const float tmin_f = f32_down(tmin);
+    constexpr uint32_t ROOM = RT_PEND_CAP - 4;  // a visit queues at most 4
+    RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
+    uint32_t pn = T.pd.n;
+    if ((T.cur != REF_NONE || T.sp > 0) && pn <= ROOM) {  // node round
+        RT_DIAG_ONLY(++dg.lane_trace_iters;)
+        if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+        const uint32_t cur = T.cur;
+        T.cur = REF_NONE;
+        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+        if (kind == K_BVH) {
+            RT_DIAG_ONLY(++dg.node_visits;)
+            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
+        } else if (kind == K_LIST) {
+            const uint32_t child = S.list_children[idx];
+            if (child != REF_NONE) {
+                if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+                T.cur = child;
+            }
+        } else if (kind == K_SPHERE) {
+            pq[pn * RT_BLOCK] = idx;
+            ++pn;
+        }
+    }
+    const bool walk = T.cur != REF_NONE || T.sp > 0;
+    const unsigned long long mw = __ballot(walk && pn <= ROOM);
+    const unsigned long long mp = __ballot(pn > 0);
+    if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH) {
+        if (pn > 0) {  // sphere round (sphere.rs:77-108)
+            RT_DIAG_ONLY(++dg.sphere_tests;)
+            --pn;
+            const uint32_t idx = pq[pn * RT_BLOCK];
+            const double4 s4 = S.spheres[idx];
+            double t;
+            if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
+                T.cl.lower(t);
+                T.found = true;
+                T.hit.t = t;
+                T.hit.ref = make_ref(K_SPHERE, idx);
+            }
+        }
+    }
+    T.pd.n = pn;
+    return walk || pn > 0;
 }
 
 // ------------------------------------------------------------------ hit record
@@ -1252,6 +1551,8 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
     __shared__ uint2 stack_lds[STACK * RT_BLOCK];
     __shared__ uint4 media_lds[TIER == TIER_FULL && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
     uint4* med = media_lds + threadIdx.x;
+    __shared__ uint32_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * RT_BLOCK : 1];
+    uint32_t* pq = pend_lds + threadIdx.x;
     StackFor<TIER> stk{stack_lds + threadIdx.x,
                        P->stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x, gridDim.x * RT_BLOCK};
     const uint32_t lane = __lane_id();
@@ -1349,20 +1650,23 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
                             : (TIER == TIER_MESH ? RT_SHADE_BATCH_MESH : RT_SHADE_BATCH_FULL);
-        if constexpr (TIER == TIER_BASIC && RT_DEFER_BASIC) {
-            trace_basic(S, ray, T, stk, dg);
-            walking = false;
-        } else if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
-            while (walking) {
-                RT_DIAG_ONLY(++dg.wave_trace_iters;)
-                walking = trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+        auto step = [&]() -> bool {
+            if constexpr (TIER == TIER_BASIC && RT_BVH4) {
+                return trace4_step(S, ray, T, stk, pq, dg);
+            } else if constexpr (TIER == TIER_BASIC && RT_SPHERE_FILTER) {
+                return trace_filtered_step(S, ray, T, stk, dg);
+            } else {
+                RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
+                return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
             }
+        };
+        if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
+            while (walking) walking = step();
             if constexpr (TIER == TIER_FULL) media_phase<TIER>(S, ray, T, stk, rng, med);
         } else {
             const unsigned long long active = __ballot(true);
             for (;;) {
-                RT_DIAG_ONLY(++dg.wave_trace_iters;)
-                if (walking) walking = trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                if (walking) walking = step();
                 const unsigned long long w = __ballot(walking);
                 if (w == 0 || __popcll(active & ~w) >= BATCH) break;
             }
@@ -1406,9 +1710,9 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
         atomicAdd(&g_diag[0], dg.cyc_refill);
         atomicAdd(&g_diag[1], dg.cyc_trace);
         atomicAdd(&g_diag[2], dg.cyc_shade);
-        atomicAdd(&g_diag[3], dg.wave_trace_iters);
         atomicAdd(&g_diag[4], dg.main_iters);
     }
+    atomicAdd(&g_diag[3], dg.wave_trace_iters);  // counted by the first active lane of each wave iteration
     atomicAdd(&g_diag[5], dg.lane_trace_iters);
     atomicAdd(&g_diag[6], dg.node_visits);
     atomicAdd(&g_diag[7], dg.sphere_tests);
@@ -1510,7 +1814,8 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     return rtk::TIER_BASIC;
 }
 
-extern "C" int rtk_nodes_boxes_only(int tier) { return tier == rtk::TIER_BASIC && RT_DEFER_BASIC; }
+extern "C" int rtk_node_sphere_f32(int tier) { return tier == rtk::TIER_BASIC && RT_SPHERE_FILTER && !RT_BVH4; }
+extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
     return tier == rtk::TIER_BASIC ? RT_STACK_BASIC : RT_STACK_MAX;

@@ -58,6 +58,10 @@ constexpr uint32_t REF_NONE = 0u;
 //    the slab test is made conservative (rt_kernel.hip slab_f), so every hit
 //    the reference's exact-box f64 test admits is admitted.
 // c1 may be REF_NONE (a BVH over one object, bvh.rs:25).
+// Basic tier with the f32 sphere filter (rt_kernel.hip sphere_filter): a sphere
+// child's slot holds the sphere rounded to nearest f32 plus g = |c|_1 + r
+// rounded up, the magnitude the filter's error bounds scale with; the exact
+// f64 sphere is read from `spheres` when the filter cannot decide.
 struct alignas(16) DNodeSlot {
     union {
         struct {
@@ -65,6 +69,11 @@ struct alignas(16) DNodeSlot {
             uint32_t pad[2];
         } box;
         double sphere[4];  // {cx, cy, cz, r}
+        struct {
+            float c[3], r;
+            float g;
+            uint32_t pad[3];
+        } fsph;
     };
 };
 struct alignas(16) DNode {
@@ -73,6 +82,16 @@ struct alignas(16) DNode {
     uint32_t pad[2];
 };
 static_assert(sizeof(DNode) == 80, "DNode must be 80 B (5 dwordx4)");
+
+// Basic-tier 4-wide BVH node (rth::bvh4_basic): up to four children, their
+// f32 boxes (rounded outward) stored component-major so one dwordx4 holds one
+// bound of all four.  A sphere child keeps the sphere filter's record in its
+// box slots instead: lo = center, hi.x = radius, hi.y = g (as DNodeSlot::fsph).
+struct alignas(16) DNode4 {
+    float lo[3][4], hi[3][4];
+    uint32_t ref[4];  // REF_NONE for an unused slot
+};
+static_assert(sizeof(DNode4) == 112, "DNode4 must be 112 B (7 dwordx4)");
 
 // Planar: quad.rs:17-27 / triangle.rs:16-26 hot fields, packed in 128 B:
 // f[0..3) unit normal, f[3] parm_d, f[4..7) anchor, f[7..10) u, f[10..13) v,
@@ -167,6 +186,7 @@ struct alignas(16) DPerlin {
 // Everything the kernel reads about the world, as device pointers.
 struct SceneView {
     const RT_GLOBAL DNode* nodes;
+    const RT_GLOBAL DNode4* nodes4;          // basic tier: K_BVH refs index these
     const RT_GLOBAL double4* spheres;        // {cx, cy, cz, r}
     const RT_GLOBAL int32_t* sphere_mat;
     const RT_GLOBAL double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}

@@ -59,6 +59,17 @@ void destroy_device_world(DeviceWorld* d) {
     delete d;
 }
 
+// The kernel tier for a flattened world, with the tier's node format applied:
+// the basic tier walks 4-wide BVH nodes (falling back to the mesh tier's
+// two-box nodes when they would need more stack than its LDS holds).
+static int prepare_tier(HostWorld& hw) {
+    int tier = rtk_tier_for(hw.features, hw.stack_need);
+    if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() && bvh4_basic(hw, RT_STACK_BASIC) > RT_STACK_BASIC)
+        tier = rtk::TIER_MESH;
+    if (rtk_node_sphere_f32(tier)) nodes_sphere_f32(hw);
+    return tier;
+}
+
 static int32_t hip_fail(hipError_t e, const char* what) {
     return set_error(RT_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -112,8 +123,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     HostWorld hw;
     int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     if (rc != RT_OK) return rc;
-    const int tier = rtk_tier_for(hw.features, hw.stack_need);
-    if (rtk_nodes_boxes_only(tier)) nodes_boxes_only(hw);
+    const int tier = prepare_tier(hw);
     const uint32_t stack_cap = rtk_stack_entries(tier);
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
@@ -130,7 +140,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
         }
     }
     std::vector<char> blob;
-    size_t o_nodes = put(blob, hw.nodes), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
+    size_t o_nodes = put(blob, hw.nodes), o_n4 = put(blob, hw.nodes4), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
            o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
            o_pl = put(blob, hw.planars), o_pla = put(blob, hw.planar_area), o_plm = put(blob, hw.planar_mat),
            o_plr = put(blob, hw.planar_remap), o_rm = put(blob, hw.remaps),
@@ -148,6 +158,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     char* b = d->blob;
     rtk::SceneView& v = d->view;
     v.nodes = (const rtk::DNode*)(b + o_nodes);
+    v.nodes4 = (const rtk::DNode4*)(b + o_n4);
     v.spheres = (const double4*)(b + o_sph);
     v.sphere_mat = (const int32_t*)(b + o_sphm);
     v.msph_center = (const double4*)(b + o_msc);
@@ -366,8 +377,10 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
         out->bvh_nodes = (uint32_t)hw.nodes.size();
         out->primitives = (uint32_t)hw.n_prims;
         out->bvh_leaves = (uint32_t)hw.n_bvh_leaves;
+        const int tier = prepare_tier(hw);
+        if (!hw.nodes4.empty()) out->bvh_nodes = (uint32_t)hw.nodes4.size();
         out->stack_need = hw.stack_need;
-        out->kernel_tier = (uint32_t)rtk_tier_for(hw.features, hw.stack_need);
+        out->kernel_tier = (uint32_t)tier;
         out->features = hw.features;
         return RT_OK;
     } catch (const std::bad_alloc&) {

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <unordered_map>
 
@@ -1053,20 +1054,151 @@ void rt_scene_destroy(rt_scene* s) {
 }  // extern "C"
 
 namespace rth {
-void nodes_boxes_only(HostWorld& hw) {
+void nodes_sphere_f32(HostWorld& hw) {
     for (rtk::DNode& n : hw.nodes) {
         const uint32_t refs[2] = {n.c0, n.c1};
         for (int k = 0; k < 2; ++k) {
             if (rtk::ref_kind(refs[k]) != rtk::K_SPHERE) continue;
             const double c[3] = {n.slot[k].sphere[0], n.slot[k].sphere[1], n.slot[k].sphere[2]};
             const double r = n.slot[k].sphere[3];
-            auto& bx = n.slot[k].box;
+            auto& fs = n.slot[k].fsph;
+            double g = 0.0;
             for (int a = 0; a < 3; ++a) {
-                bx.lo[a] = round_down(c[a] - r);
-                bx.hi[a] = round_up(c[a] + r);
+                fs.c[a] = (float)c[a];
+                g += std::fabs((double)fs.c[a]);
             }
-            bx.pad[0] = bx.pad[1] = 0;
+            fs.r = (float)r;
+            fs.g = round_up(g + std::fabs((double)fs.r));
+            fs.pad[0] = fs.pad[1] = fs.pad[2] = 0;
         }
     }
+}
+}  // namespace rth
+
+namespace rth {
+// Collapses the two-box BVHs of a basic-tier world into 4-wide nodes: starting
+// from a node's two children, the inner child with the largest box (surface
+// area) is replaced by its own children until there are four or no inner child
+// is left (the usual top-down BVH2 -> BVH4 collapse).  Child boxes are the
+// parents' f32 boxes, already rounded outward; sphere children become filter
+// records.  Stack need: a visit pushes all hit inner children but the nearest,
+// so need(node) = (inner children - 1) + max need(inner child); queued
+// spheres use no stack entries.
+uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
+    using rtk::REF_NONE;
+    struct Child {
+        uint32_t ref;
+        float lo[3], hi[3];
+        double area;
+    };
+    std::vector<rtk::DNode4> out;
+    std::vector<uint32_t> map(hw.nodes.size(), REF_NONE);
+    auto kids = [&](uint32_t idx, std::vector<Child>& v) {
+        const rtk::DNode& n = hw.nodes[idx];
+        const uint32_t refs[2] = {n.c0, n.c1};
+        for (int k = 0; k < 2; ++k) {
+            if (refs[k] == REF_NONE) continue;
+            Child c{};
+            c.ref = refs[k];
+            if (rtk::ref_kind(refs[k]) == rtk::K_SPHERE) {
+                c.area = -1.0;
+            } else {
+                for (int a = 0; a < 3; ++a) {
+                    c.lo[a] = n.slot[k].box.lo[a];
+                    c.hi[a] = n.slot[k].box.hi[a];
+                }
+                const double dx = std::fmax((double)c.hi[0] - c.lo[0], 0.0), dy = std::fmax((double)c.hi[1] - c.lo[1], 0.0),
+                             dz = std::fmax((double)c.hi[2] - c.lo[2], 0.0);
+                c.area = dx * dy + dy * dz + dz * dx;
+            }
+            v.push_back(c);
+        }
+    };
+    std::function<uint32_t(uint32_t)> conv = [&](uint32_t idx) -> uint32_t {
+        if (map[idx] != REF_NONE) return map[idx];
+        std::vector<Child> ch;
+        kids(idx, ch);
+        for (;;) {
+            if (ch.size() >= 4) break;
+            int best = -1;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (rtk::ref_kind(ch[i].ref) == rtk::K_BVH && (best < 0 || ch[i].area > ch[best].area)) best = (int)i;
+            if (best < 0) break;
+            std::vector<Child> sub;
+            kids(rtk::ref_index(ch[best].ref), sub);
+            ch.erase(ch.begin() + best);
+            ch.insert(ch.begin() + best, sub.begin(), sub.end());
+        }
+        const uint32_t at = (uint32_t)out.size();
+        out.emplace_back();
+        map[idx] = rtk::make_ref(rtk::K_BVH, at);
+        rtk::DNode4 n{};
+        for (int i = 0; i < 4; ++i) {
+            n.ref[i] = REF_NONE;
+            for (int a = 0; a < 3; ++a) {
+                n.lo[a][i] = 1.0f;  // empty slot: inverted box, and masked by its REF_NONE
+                n.hi[a][i] = 0.0f;
+            }
+        }
+        for (size_t i = 0; i < ch.size(); ++i) {
+            uint32_t r = ch[i].ref;
+            if (rtk::ref_kind(r) == rtk::K_SPHERE) {
+                const double4 sp = hw.spheres[rtk::ref_index(r)];
+                const float c[3] = {(float)sp.x, (float)sp.y, (float)sp.z}, rad = (float)sp.w;
+                for (int a = 0; a < 3; ++a) n.lo[a][i] = c[a];
+                n.hi[0][i] = rad;
+                n.hi[1][i] = round_up(std::fabs((double)c[0]) + std::fabs((double)c[1]) + std::fabs((double)c[2]) +
+                                      std::fabs((double)rad));
+                n.hi[2][i] = 0.0f;
+            } else {
+                if (rtk::ref_kind(r) == rtk::K_BVH) r = conv(rtk::ref_index(r));
+                for (int a = 0; a < 3; ++a) {
+                    n.lo[a][i] = ch[i].lo[a];
+                    n.hi[a][i] = ch[i].hi[a];
+                }
+            }
+            n.ref[i] = r;
+        }
+        out[at] = n;
+        return map[idx];
+    };
+    std::vector<uint32_t> lists = hw.list_children;
+    for (uint32_t& r : lists)
+        if (rtk::ref_kind(r) == rtk::K_BVH) r = conv(rtk::ref_index(r));
+    uint32_t root = hw.world_root;
+    if (rtk::ref_kind(root) == rtk::K_BVH) root = conv(rtk::ref_index(root));
+    // stack need of a ref in the converted world
+    std::unordered_map<uint32_t, uint32_t> memo;
+    std::function<uint32_t(uint32_t)> need = [&](uint32_t r) -> uint32_t {
+        const uint32_t kind = rtk::ref_kind(r), idx = rtk::ref_index(r);
+        if (kind != rtk::K_BVH && kind != rtk::K_LIST) return 0;
+        auto it = memo.find(r);
+        if (it != memo.end()) return it->second;
+        uint32_t v = 0;
+        if (kind == rtk::K_BVH) {
+            uint32_t inner = 0, deepest = 0;
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t c = out[idx].ref[i];
+                if (c == REF_NONE || rtk::ref_kind(c) == rtk::K_SPHERE) continue;
+                ++inner;
+                deepest = std::max(deepest, need(c));
+            }
+            v = inner ? (inner - 1) + deepest : 0;
+        } else {  // iterator form: popping (LIST,p) pushes (LIST,p+1) then walks child p
+            for (uint32_t p = idx; lists[p] != REF_NONE; ++p) {
+                const bool last = lists[p + 1] == REF_NONE;
+                v = std::max(v, (last ? 0u : 1u) + need(lists[p]));
+            }
+        }
+        memo[r] = v;
+        return v;
+    };
+    const uint32_t sn = 1 + need(root);
+    if (sn > max_need) return sn;
+    hw.nodes4 = std::move(out);
+    hw.list_children = std::move(lists);
+    hw.world_root = root;
+    hw.stack_need = sn;
+    return sn;
 }
 }  // namespace rth

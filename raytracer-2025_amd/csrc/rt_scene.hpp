@@ -107,6 +107,7 @@ struct MatRec {
 // Flattened world on the host, ready to upload as one blob.
 struct HostWorld {
     std::vector<rtk::DNode> nodes;
+    std::vector<rtk::DNode4> nodes4;  // basic tier (bvh4_basic)
     std::vector<double4> spheres;
     std::vector<int32_t> sphere_mat;
     std::vector<double4> msph_center, msph_dir;
@@ -154,9 +155,15 @@ int32_t set_error(int32_t code, const std::string& msg);
 // the binned-SAH rebuild (closest-hit results agree up to exact t ties).
 int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, bool reference_bvh,
                 HostWorld& out);
-// Rewrites every sphere child slot of every BVH node as the sphere's f32 box
-// (rounded outward): the node format of kernel tiers that queue sphere tests
-// instead of running them inside the node visit (rtk_nodes_boxes_only).
-void nodes_boxes_only(HostWorld& hw);
+// Rewrites every sphere child slot of every BVH node as the f32 record of the
+// basic tier's sphere filter (DNodeSlot::fsph: center and radius rounded to
+// nearest, g = |c|_1 + r rounded up): the node format of kernels that test
+// spheres in f32 first and queue the exact f64 test (rtk_node_sphere_f32).
+void nodes_sphere_f32(HostWorld& hw);
+// Basic tier: collapses every two-box BVH into 4-wide nodes (hw.nodes4, sphere
+// children as filter records), rewrites the K_BVH refs to index nodes4 and
+// recomputes stack_need.  Returns the new stack_need (hw is unchanged when it
+// exceeds max_need).
+uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need);
 void destroy_device_world(DeviceWorld* d);
 }  // namespace rth

@@ -41,6 +41,7 @@ for n in names:
         world, lights, cam = scenes.obj_terrain(scene, obj, 1920, spp)
     else:
         world, lights, cam = scenes.random_spheres(scene, 1920, spp)
+    print("warm-up", n, file=sys.stderr, flush=True)
     lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)  # warm-up
     runs[n] = (scene, world, lights, cam, lin)
 res = {n: [] for n in names}
@@ -49,6 +50,7 @@ for _ in range(reps):
         scene, world, lights, cam, ref = runs[n]
         lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)
         res[n].append(st.kernel_ms)
+        print(n, st.kernel_ms, file=sys.stderr, flush=True)
 base = runs[names[0]][4]
 out = {}
 for n in names:

@@ -18,7 +18,7 @@ rt = importlib.import_module("raytracer-2025_amd.raytracer")
 scenes = importlib.import_module("raytracer-2025_amd.scenes")
 
 torch.cuda.init()
-lib = ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", "librt_mi355x_diag.so"))
+lib = ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", os.environ.get("DIAG_LIB", "librt_mi355x_diag.so")))
 api = capi.Api(lib, "rt_")
 lib.rt_diag_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
@@ -53,7 +53,7 @@ out = {
     "trace_iters_per_ray": c[5] / c[8],
     "wave_trace_iters_per_wave_bounce": c[3] / max(1, c[4]),
     "node_visits_per_ray": c[6] / c[8],
-    "sphere_tests_per_ray(not inlined)": c[7] / c[8],
+    "queued_f64_sphere_tests_per_ray": c[7] / c[8],
     "raw": c[:9],
 }
 print(json.dumps(out, indent=1))
