@@ -43,7 +43,8 @@ def main(rnd="r01", src="gpurun_out/box"):
     src = os.path.join(ROOT, src)
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    summary = {}
+    old = os.path.join(dst, "pmc_summary.json")
+    summary = json.load(open(old)) if os.path.exists(old) else {}  # workloads this run did not profile keep theirs
     for w in ("c2", "c3", "c4", "c5"):
         entry = {}
         ks = os.path.join(src, "trace_" + w, "run_kernel_stats.csv")
@@ -70,7 +71,8 @@ def main(rnd="r01", src="gpurun_out/box"):
             lines = [l for l in open(bl) if l.startswith("{")]
             if lines:
                 open(os.path.join(dst, "bench_%s.json" % w), "w").write(lines[-1])
-        summary[w] = entry
+        if entry.get("per_launch") or "kernel" in entry or w not in summary:
+            summary[w] = entry
     json.dump(summary, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
