@@ -34,6 +34,10 @@ namespace rtk {
 #define RT_BVH4 1
 #endif
 #define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
+// Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
+#ifndef RT_MESH_BVH4
+#define RT_MESH_BVH4 1
+#endif
 
 // Diagnostic build (-DRT_DIAG, librt_mi355x_diag.so only): per-wave cycle
 // stamps and per-lane work counters, summed into g_diag.  The product build
@@ -765,7 +769,9 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
     if (kind == K_BVH) {
-        if constexpr (TIER == TIER_BASIC && RT_BRANCHLESS)
+        if constexpr (TIER == TIER_MESH && RT_MESH_BVH4)
+            T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
+        else if constexpr (TIER == TIER_BASIC && RT_BRANCHLESS)
             T.cur = visit_node_sel(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, T.found, T.hit, stk, T.sp);
         else
             T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
@@ -1048,6 +1054,49 @@ __device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, con
         ref[i] = R[i];
     }
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
+        const bool sw = key[b] < key[a];
+        const float ka = key[a], kb = key[b];
+        const uint32_t ra = ref[a], rb = ref[b];
+        key[a] = sw ? kb : ka;
+        key[b] = sw ? ka : kb;
+        ref[a] = sw ? rb : ra;
+        ref[b] = sw ? ra : rb;
+    };
+    cs(0, 1);
+    cs(2, 3);
+    cs(0, 2);
+    cs(1, 3);
+    cs(1, 2);
+    if (key[3] < INF) stk.push(sp++, ref[3], key[3]);
+    if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
+    if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
+    return key[0] < INF ? ref[0] : REF_NONE;
+}
+
+// One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
+// tests, the hit children sorted by entry distance, the nearest walked next
+// and the others pushed farthest first -- primitives included, so a triangle
+// is tested (planar_t) when the walk reaches it, in distance order.
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
+                                                 float c_f, Stack& stk, uint32_t& sp) {
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
+    const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], rq = np[6];
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
+    const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
+    constexpr float INF = __builtin_huge_valf();
+    float key[4];
+    uint32_t ref[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float lo[3] = {LX[i], LY[i], LZ[i]}, hi[3] = {HX[i], HY[i], HZ[i]};
+        float e;
+        const bool h = slab_f(lo, hi, rf, tmin_f, c_f, e) && R[i] != REF_NONE;
+        key[i] = h ? e : INF;
+        ref[i] = R[i];
+    }
+    auto cs = [&](int a, int b) {
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];
         const uint32_t ra = ref[a], rb = ref[b];
@@ -1523,7 +1572,10 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_SHADE_BATCH_FULL 64
 #endif
 #ifndef RT_QUEUE_CHUNK
-#define RT_QUEUE_CHUNK 256  // items a wave takes per queue atomic (>= 64)
+#define RT_QUEUE_CHUNK 256  // most items a wave takes per queue atomic (>= 64)
+#endif
+#ifndef RT_QUEUE_GUIDE
+#define RT_QUEUE_GUIDE 8  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
 #endif
 #ifndef RT_MESH_WAVES
 #define RT_MESH_WAVES 4  // 4-wave budget (some spills) beats 2 waves: 164.7 vs 263.8 ms (C4, 64 spp)
@@ -1583,15 +1635,26 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
             const uint32_t n = (uint32_t)__popcll(mask);
             const uint32_t avail = pool_end - pool_next;
             uint32_t fresh = 0;
+            // guided chunk: about 1/GUIDE of the items left (as last seen) per
+            // wave of the grid, so the last chunks are small and waves finish
+            // together; never below 64 (one item per lane)
+            uint32_t chunk = RT_QUEUE_CHUNK;
+#if RT_QUEUE_GUIDE
+            {
+                const uint32_t left = F.total_items > pool_end ? F.total_items - pool_end : 0u;
+                const uint32_t g = left / (gridDim.x * (RT_BLOCK / 64) * RT_QUEUE_GUIDE);
+                chunk = g < 64u ? 64u : (g > (uint32_t)RT_QUEUE_CHUNK ? (uint32_t)RT_QUEUE_CHUNK : g);
+            }
+#endif
             if (avail < n) {
                 const uint32_t leader = __ffsll((long long)mask) - 1;
-                if (lane == leader) fresh = atomicAdd(queue, (uint32_t)RT_QUEUE_CHUNK);
+                if (lane == leader) fresh = atomicAdd(queue, chunk);
                 fresh = __shfl(fresh, leader);
             }
             const uint32_t old_next = pool_next;
             if (avail < n) {
                 pool_next = fresh + (n - avail);
-                pool_end = fresh + RT_QUEUE_CHUNK;
+                pool_end = fresh + chunk;
             } else {
                 pool_next += n;
             }
@@ -1816,6 +1879,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 
 extern "C" int rtk_node_sphere_f32(int tier) { return tier == rtk::TIER_BASIC && RT_SPHERE_FILTER && !RT_BVH4; }
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
+extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
     return tier == rtk::TIER_BASIC ? RT_STACK_BASIC : RT_STACK_MAX;

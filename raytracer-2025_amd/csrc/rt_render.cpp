@@ -60,12 +60,16 @@ void destroy_device_world(DeviceWorld* d) {
 }
 
 // The kernel tier for a flattened world, with the tier's node format applied:
-// the basic tier walks 4-wide BVH nodes (falling back to the mesh tier's
-// two-box nodes when they would need more stack than its LDS holds).
+// the basic and mesh tiers walk 4-wide BVH nodes; a world whose 4-wide nodes
+// would need more stack than the tier holds moves up a tier (the basic tier's
+// LDS stack -> the mesh tier; the mesh tier's LDS + overflow stack -> the full
+// tier, which walks two-box nodes).
 static int prepare_tier(HostWorld& hw) {
     int tier = rtk_tier_for(hw.features, hw.stack_need);
-    if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() && bvh4_basic(hw, RT_STACK_BASIC) > RT_STACK_BASIC)
+    if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() && bvh4_convert(hw, RT_STACK_BASIC, true) > RT_STACK_BASIC)
         tier = rtk::TIER_MESH;
+    if (tier == rtk::TIER_MESH && rtk_mesh_bvh4() && bvh4_convert(hw, RT_STACK_MAX, false) > RT_STACK_MAX)
+        tier = rtk::TIER_FULL;
     if (rtk_node_sphere_f32(tier)) nodes_sphere_f32(hw);
     return tier;
 }

@@ -1076,15 +1076,16 @@ void nodes_sphere_f32(HostWorld& hw) {
 }  // namespace rth
 
 namespace rth {
-// Collapses the two-box BVHs of a basic-tier world into 4-wide nodes: starting
-// from a node's two children, the inner child with the largest box (surface
-// area) is replaced by its own children until there are four or no inner child
-// is left (the usual top-down BVH2 -> BVH4 collapse).  Child boxes are the
-// parents' f32 boxes, already rounded outward; sphere children become filter
-// records.  Stack need: a visit pushes all hit inner children but the nearest,
-// so need(node) = (inner children - 1) + max need(inner child); queued
-// spheres use no stack entries.
-uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
+// Collapses the two-box BVHs of a world into 4-wide nodes: starting from a
+// node's two children, the inner child with the largest box (surface area) is
+// replaced by its own children until there are four or no inner child is left
+// (the usual top-down BVH2 -> BVH4 collapse).  Child boxes are the parents' f32
+// boxes, already rounded outward.  filter_spheres (basic tier): sphere children
+// become filter records and are queued, not stacked, so need(node) = (inner
+// children - 1) + max need(inner child); otherwise (mesh tier) a sphere child
+// gets its box rounded outward and, like every child, is walked near-first
+// through the stack: need(node) = (children - 1) + max need(child).
+uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres) {
     using rtk::REF_NONE;
     struct Child {
         uint32_t ref;
@@ -1102,6 +1103,11 @@ uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
             c.ref = refs[k];
             if (rtk::ref_kind(refs[k]) == rtk::K_SPHERE) {
                 c.area = -1.0;
+                const double* sp = n.slot[k].sphere;
+                for (int a = 0; a < 3; ++a) {
+                    c.lo[a] = round_down(sp[a] - sp[3]);
+                    c.hi[a] = round_up(sp[a] + sp[3]);
+                }
             } else {
                 for (int a = 0; a < 3; ++a) {
                     c.lo[a] = n.slot[k].box.lo[a];
@@ -1142,7 +1148,7 @@ uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
         }
         for (size_t i = 0; i < ch.size(); ++i) {
             uint32_t r = ch[i].ref;
-            if (rtk::ref_kind(r) == rtk::K_SPHERE) {
+            if (filter_spheres && rtk::ref_kind(r) == rtk::K_SPHERE) {
                 const double4 sp = hw.spheres[rtk::ref_index(r)];
                 const float c[3] = {(float)sp.x, (float)sp.y, (float)sp.z}, rad = (float)sp.w;
                 for (int a = 0; a < 3; ++a) n.lo[a][i] = c[a];
@@ -1179,7 +1185,7 @@ uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
             uint32_t inner = 0, deepest = 0;
             for (int i = 0; i < 4; ++i) {
                 const uint32_t c = out[idx].ref[i];
-                if (c == REF_NONE || rtk::ref_kind(c) == rtk::K_SPHERE) continue;
+                if (c == REF_NONE || (filter_spheres && rtk::ref_kind(c) == rtk::K_SPHERE)) continue;
                 ++inner;
                 deepest = std::max(deepest, need(c));
             }
@@ -1196,6 +1202,7 @@ uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need) {
     const uint32_t sn = 1 + need(root);
     if (sn > max_need) return sn;
     hw.nodes4 = std::move(out);
+    hw.nodes.clear();  // the two-box nodes are not walked any more
     hw.list_children = std::move(lists);
     hw.world_root = root;
     hw.stack_need = sn;

@@ -160,10 +160,10 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 // nearest, g = |c|_1 + r rounded up): the node format of kernels that test
 // spheres in f32 first and queue the exact f64 test (rtk_node_sphere_f32).
 void nodes_sphere_f32(HostWorld& hw);
-// Basic tier: collapses every two-box BVH into 4-wide nodes (hw.nodes4, sphere
-// children as filter records), rewrites the K_BVH refs to index nodes4 and
-// recomputes stack_need.  Returns the new stack_need (hw is unchanged when it
-// exceeds max_need).
-uint32_t bvh4_basic(HostWorld& hw, uint32_t max_need);
+// Collapses every two-box BVH into 4-wide nodes (hw.nodes4; sphere children as
+// filter records when filter_spheres, the basic tier), rewrites the K_BVH refs
+// to index nodes4 and recomputes stack_need.  Returns the new stack_need (hw is
+// unchanged when it exceeds max_need).
+uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres);
 void destroy_device_world(DeviceWorld* d);
 }  // namespace rth
