@@ -11,7 +11,7 @@
 #define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
-#define RT_STACK_MAX 64     // LDS + overflow entries (mesh and full tiers)
+#define RT_STACK_MAX 96     // LDS + overflow entries (mesh and full tiers)
 #ifndef RT_MEDIA_CAP
 #define RT_MEDIA_CAP 2      // full tier: media a walk queues (in LDS, 16 B each) before testing them inline
 #endif
@@ -23,7 +23,11 @@ namespace rtk {
 //  MESH:  BASIC + quads / triangles + OBJ RemappedMaterial (C4);
 //  FULL:  everything (transforms, media, moving spheres, lights, all materials
 //         and textures: C3, C5).
-enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2 };
+//  FULL_FLAT: FULL for worlds without any BVH node (C3): the walk carries no
+//         BVH code, which leaves the registers to the rest (fewer spills).
+enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2, TIER_FULL_FLAT = 3 };
+constexpr int N_TIERS = 4;
+__host__ __device__ constexpr bool tier_full(int t) { return t >= TIER_FULL; }
 }  // namespace rtk
 
 // Camera::initilize results (camera.rs:204-245) for one shard.
@@ -46,6 +50,7 @@ extern "C" int rtk_node_sphere_f32(int tier);
 extern "C" int rtk_basic_bvh4(void);
 // 1 if the mesh tier's kernel walks 4-wide BVH nodes with every child boxed
 extern "C" int rtk_mesh_bvh4(void);
+extern "C" int rtk_full_bvh4(void);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
                                        int toon, hipStream_t stream, int tier, int grid, void* params_dev,

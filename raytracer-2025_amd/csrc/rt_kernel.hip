@@ -38,6 +38,10 @@ namespace rtk {
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
 #endif
+// Full tier: the same boxed 4-wide nodes, for the walk and the medium boundary walks.
+#ifndef RT_FULL_BVH4
+#define RT_FULL_BVH4 1
+#endif
 
 // Diagnostic build (-DRT_DIAG, librt_mi355x_diag.so only): per-wave cycle
 // stamps and per-lane work counters, summed into g_diag.  The product build
@@ -372,7 +376,7 @@ struct StackT {
     }
 };
 template <int TIER>
-using StackFor = StackT<TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
+using StackFor = StackT<tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
                         TIER != TIER_BASIC>;
 __device__ __forceinline__ float f32_down(double x) {
     float f = (float)x;  // round-to-nearest; step one ulp down when it rounded up
@@ -523,7 +527,7 @@ constexpr float NO_CULL = -__builtin_huge_valf();
 
 // Closest t of a medium boundary (no media inside, no records) -- the two
 // boundary.hit calls of volume.rs:44-48.
-template <class Stack>
+template <bool BVH, class Stack>
 __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, double tmin, double tmax, Stack& stk,
                            uint32_t sp0, double& tbest) {
     Ray r = r0;
@@ -547,7 +551,14 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
         cur = REF_NONE;
         double t;
         switch (kind) {
-            case K_BVH: cur = visit_node(S, idx, r, rf, a, inva, tmin, tmin_f, cl, stk, sp, on_hit); break;
+            case K_BVH:
+                if constexpr (!BVH)
+                    break;
+                else if constexpr (RT_FULL_BVH4)
+                    cur = visit4_boxes(S, idx, rf, tmin_f, cl.c_f, stk, sp);
+                else
+                    cur = visit_node(S, idx, r, rf, a, inva, tmin, tmin_f, cl, stk, sp, on_hit);
+                break;
             case K_LIST: {
                 const uint32_t child = S.list_children[idx];
                 if (child != REF_NONE) {
@@ -610,7 +621,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // ConstantMedium::hit (volume.rs:37-73) of medium idx for ray r in the
 // medium's frame, interval [tmin, tmax]: the two boundary hits are one
 // boundary walk run twice (one copy of the walk in the code).
-template <class Stack>
+template <bool BVH, class Stack>
 __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, const Ray& r, double tmin, double tmax,
                                            Stack& stk, uint32_t sp0, const Rng& rng, double& t) {
     const DMedium M = S.media[idx];
@@ -619,7 +630,7 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
 #pragma nounroll
     for (int pass = 0; pass < 2; ++pass) {
         double tb;
-        if (!boundary_t(S, M.boundary, r, lo, PINF, stk, sp0, tb)) return false;
+        if (!boundary_t<BVH>(S, M.boundary, r, lo, PINF, stk, sp0, tb)) return false;
         if (pass == 0) {
             t1 = tb;
             lo = fmin(t1 + 0.0001, PINF);
@@ -737,7 +748,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
 template <int TIER>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
                                            const Rng& rng, uint4* med, Diag& dg) {
-    constexpr bool FULL = TIER == TIER_FULL;
+    constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
     if (T.cur == REF_NONE) {
@@ -768,8 +779,8 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         }
     };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
-    if (kind == K_BVH) {
-        if constexpr (TIER == TIER_MESH && RT_MESH_BVH4)
+    if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
+        if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (TIER == TIER_FULL && RT_FULL_BVH4))
             T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
         else if constexpr (TIER == TIER_BASIC && RT_BRANCHLESS)
             T.cur = visit_node_sel(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, T.found, T.hit, stk, T.sp);
@@ -826,7 +837,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                     med[T.nmed * RT_BLOCK] = make_uint4(idx, T.nxf, T.xfs.a, T.xfs.b);
                     ++T.nmed;
                 } else {
-                    got = medium_hit(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
+                    got = medium_hit<TIER != TIER_FULL_FLAT>(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
                 }
                 break;
             }
@@ -850,7 +861,7 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, T
         Ray r = wr;
         for (uint32_t j = 0; j < e.y; ++j) r = xf_ray(S.xforms[j == 0 ? e.z : e.w], r);
         double t;
-        if (medium_hit(S, e.x, r, 1e-8, T.cl.c, stk, 0, rng, t)) {
+        if (medium_hit<TIER != TIER_FULL_FLAT>(S, e.x, r, 1e-8, T.cl.c, stk, 0, rng, t)) {
             T.cl.set(t);
             T.found = true;
             T.hit.t = t;
@@ -1181,7 +1192,7 @@ struct Rec {
 // its innermost Transform, then carried out through the chain (shapes.rs:104-108).
 template <int TIER>
 __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, bool& panic) {
-    constexpr bool FULL = TIER == TIER_FULL, PLANAR = TIER >= TIER_MESH;
+    constexpr bool FULL = tier_full(TIER), PLANAR = TIER >= TIER_MESH;
     Ray r = wr;
     if constexpr (FULL)
         for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf.get(k)], r);
@@ -1369,7 +1380,7 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 template <int TIER>
 __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
                                       const HitInfo& h, bool& panic) {
-    constexpr bool FULL = TIER == TIER_FULL;
+    constexpr bool FULL = tier_full(TIER);
     uint32_t ovf = 0;
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
@@ -1593,15 +1604,15 @@ struct KParams {
 };
 
 template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+__global__ void __launch_bounds__(RT_BLOCK, tier_full(TIER) ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
     const Frame& F = P->F;
     uint32_t* queue = P->queue;
-    constexpr int STACK = TIER == TIER_FULL ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
+    constexpr int STACK = tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
     __shared__ uint2 stack_lds[STACK * RT_BLOCK];
-    __shared__ uint4 media_lds[TIER == TIER_FULL && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
+    __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
     uint4* med = media_lds + threadIdx.x;
     __shared__ uint32_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * RT_BLOCK : 1];
     uint32_t* pq = pend_lds + threadIdx.x;
@@ -1725,7 +1736,7 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
         };
         if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
             while (walking) walking = step();
-            if constexpr (TIER == TIER_FULL) media_phase<TIER>(S, ray, T, stk, rng, med);
+            if constexpr (tier_full(TIER)) media_phase<TIER>(S, ray, T, stk, rng, med);
         } else {
             const unsigned long long active = __ballot(true);
             for (;;) {
@@ -1735,7 +1746,7 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL ? RT_FULL_WAVES : 
             }
         }
         RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
-        if constexpr (BATCH < 64 && TIER == TIER_FULL) {
+        if constexpr (BATCH < 64 && tier_full(TIER)) {
             if (!walking) media_phase<TIER>(S, ray, T, stk, rng, med);
         }
         if (BATCH < 64 && walking) continue;
@@ -1810,15 +1821,20 @@ RT_TIER_ENTRY(1)
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 2
 RT_TIER_ENTRY(2)
 #endif
+#if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 3
+RT_TIER_ENTRY(3)
+#endif
 #endif
 
 #if !defined(RT_TIER_ONLY)
 extern "C" hipError_t rtk_launch_path_0(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_1(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_2(int, hipStream_t, const rtk::KParams*);
+extern "C" hipError_t rtk_launch_path_3(int, hipStream_t, const rtk::KParams*);
 extern "C" int rtk_occupancy_0(int*);
 extern "C" int rtk_occupancy_1(int*);
 extern "C" int rtk_occupancy_2(int*);
+extern "C" int rtk_occupancy_3(int*);
 
 namespace rtk {
 // Color::to_rgb (utils/color.rs:14-36): optional ACES fit, clamp, then the sRGB
@@ -1880,6 +1896,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 extern "C" int rtk_node_sphere_f32(int tier) { return tier == rtk::TIER_BASIC && RT_SPHERE_FILTER && !RT_BVH4; }
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }
+extern "C" int rtk_full_bvh4(void) { return RT_FULL_BVH4; }
 
 extern "C" uint32_t rtk_stack_entries(int tier) {
     return tier == rtk::TIER_BASIC ? RT_STACK_BASIC : RT_STACK_MAX;
@@ -1922,7 +1939,8 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
     e = tier == rtk::TIER_BASIC  ? rtk_launch_path_0(grid, stream, Pd)
         : tier == rtk::TIER_MESH ? rtk_launch_path_1(grid, stream, Pd)
-                                 : rtk_launch_path_2(grid, stream, Pd);
+        : tier == rtk::TIER_FULL ? rtk_launch_path_2(grid, stream, Pd)
+                                 : rtk_launch_path_3(grid, stream, Pd);
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
@@ -1953,6 +1971,7 @@ extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
     return tier == rtk::TIER_BASIC  ? rtk_occupancy_0(blocks_per_cu)
          : tier == rtk::TIER_MESH ? rtk_occupancy_1(blocks_per_cu)
-                                  : rtk_occupancy_2(blocks_per_cu);
+         : tier == rtk::TIER_FULL ? rtk_occupancy_2(blocks_per_cu)
+                                  : rtk_occupancy_3(blocks_per_cu);
 }
 #endif  // !RT_TIER_ONLY

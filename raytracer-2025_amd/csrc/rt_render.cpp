@@ -37,7 +37,7 @@ struct DeviceWorld {
     uint64_t pending_samples = 0;
     double pending_flatten_ms = 0;
     std::chrono::steady_clock::time_point pending_t0;
-    int grid[3] = {0, 0, 0};
+    int grid[rtk::N_TIERS] = {};
     int tier = 1;
     int cus = 0;
     bool reference_bvh = false;
@@ -62,14 +62,23 @@ void destroy_device_world(DeviceWorld* d) {
 // The kernel tier for a flattened world, with the tier's node format applied:
 // the basic and mesh tiers walk 4-wide BVH nodes; a world whose 4-wide nodes
 // would need more stack than the tier holds moves up a tier (the basic tier's
-// LDS stack -> the mesh tier; the mesh tier's LDS + overflow stack -> the full
-// tier, which walks two-box nodes).
+// LDS stack -> the mesh tier -> the full tier, whose walk has no fallback:
+// -1 with RT_ESTACK set).
 static int prepare_tier(HostWorld& hw) {
     int tier = rtk_tier_for(hw.features, hw.stack_need);
     if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() && bvh4_convert(hw, RT_STACK_BASIC, true) > RT_STACK_BASIC)
         tier = rtk::TIER_MESH;
     if (tier == rtk::TIER_MESH && rtk_mesh_bvh4() && bvh4_convert(hw, RT_STACK_MAX, false) > RT_STACK_MAX)
         tier = rtk::TIER_FULL;
+    if (tier == rtk::TIER_FULL && hw.nodes.empty()) return rtk::TIER_FULL_FLAT;
+    if (tier == rtk::TIER_FULL && rtk_full_bvh4()) {
+        const uint32_t need = bvh4_convert(hw, RT_STACK_MAX, false);
+        if (need > RT_STACK_MAX) {
+            set_error(RT_ESTACK, "world needs " + std::to_string(need) + " traversal-stack entries, kernel has " +
+                                     std::to_string(RT_STACK_MAX));
+            return -1;
+        }
+    }
     if (rtk_node_sphere_f32(tier)) nodes_sphere_f32(hw);
     return tier;
 }
@@ -112,7 +121,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
         if ((e = hipMalloc(&d->params, rtk_params_bytes())) != hipSuccess) return hip_fail(e, "hipMalloc params");
         if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
         if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        for (int t = 0; t < 3; ++t) {
+        for (int t = 0; t < rtk::N_TIERS; ++t) {
             int bpc = 0;
             if ((e = (hipError_t)rtk_path_kernel_occupancy(t, &bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
             if (bpc < 1) bpc = 1;
@@ -128,6 +137,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     if (rc != RT_OK) return rc;
     const int tier = prepare_tier(hw);
+    if (tier < 0) return RT_ESTACK;
     const uint32_t stack_cap = rtk_stack_entries(tier);
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
@@ -382,6 +392,7 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
         out->primitives = (uint32_t)hw.n_prims;
         out->bvh_leaves = (uint32_t)hw.n_bvh_leaves;
         const int tier = prepare_tier(hw);
+        if (tier < 0) return RT_ESTACK;
         if (!hw.nodes4.empty()) out->bvh_nodes = (uint32_t)hw.nodes4.size();
         out->stack_need = hw.stack_need;
         out->kernel_tier = (uint32_t)tier;

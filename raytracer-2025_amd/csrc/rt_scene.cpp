@@ -1173,10 +1173,18 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres) {
         if (rtk::ref_kind(r) == rtk::K_BVH) r = conv(rtk::ref_index(r));
     uint32_t root = hw.world_root;
     if (rtk::ref_kind(root) == rtk::K_BVH) root = conv(rtk::ref_index(root));
+    std::vector<rtk::DXform> xforms = hw.xforms;
+    for (rtk::DXform& x : xforms)
+        if (rtk::ref_kind(x.child) == rtk::K_BVH) x.child = conv(rtk::ref_index(x.child));
+    std::vector<rtk::DMedium> media = hw.media;
+    for (rtk::DMedium& m : media)
+        if (rtk::ref_kind(m.boundary) == rtk::K_BVH) m.boundary = conv(rtk::ref_index(m.boundary));
     // stack need of a ref in the converted world
     std::unordered_map<uint32_t, uint32_t> memo;
     std::function<uint32_t(uint32_t)> need = [&](uint32_t r) -> uint32_t {
         const uint32_t kind = rtk::ref_kind(r), idx = rtk::ref_index(r);
+        if (kind == rtk::K_XFORM) return 1 + need(xforms[idx].child);  // + its POPXF marker
+        if (kind == rtk::K_MEDIUM) return need(media[idx].boundary);    // boundary walks from the same sp
         if (kind != rtk::K_BVH && kind != rtk::K_LIST) return 0;
         auto it = memo.find(r);
         if (it != memo.end()) return it->second;
@@ -1204,6 +1212,8 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres) {
     hw.nodes4 = std::move(out);
     hw.nodes.clear();  // the two-box nodes are not walked any more
     hw.list_children = std::move(lists);
+    hw.xforms = std::move(xforms);
+    hw.media = std::move(media);
     hw.world_root = root;
     hw.stack_need = sn;
     return sn;
