@@ -191,6 +191,8 @@ def main():
         api.check(api.render_device_wait(scene.s, ctypes.byref(st)))  # HIP events around the path kernel
         if record:
             kernel_ms.append(st.kernel_ms)
+        if rank == 0 and st.kernel_ms > 5000.0:  # long frames (C5 on few GPUs): show progress
+            print("bench.py: frame %.1f s" % (st.kernel_ms / 1e3), file=sys.stderr, flush=True)
         if distributed:
             shard = out[:rows] if args.backend == "nccl" else out[:rows].cpu()
             frame = pdist.gather_frame(shard, H, W)

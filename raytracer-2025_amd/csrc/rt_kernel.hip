@@ -1569,6 +1569,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #ifndef RT_FULL_WAVES
 #define RT_FULL_WAVES 3  // 3 waves with some spills beat 2 without: C3 -13 %, C5 -19 %
 #endif
+#ifndef RT_FLAT_WAVES
+#define RT_FLAT_WAVES 3  // FULL_FLAT
+#endif
 // Lanes of a wave that must have finished their walk before it shades (64 =
 // all).  Trace-heavy worlds (deep triangle BVHs) gain from shading in batches;
 // for C2 the shading divergence of small batches costs more than the walks
@@ -1604,7 +1607,7 @@ struct KParams {
 };
 
 template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, tier_full(TIER) ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;

@@ -21,6 +21,7 @@ run() {  # name timeout cmd...
 run bench_c2 400 python3 bench.py
 run bench_c4 600 python3 bench.py --workload c4 --steps 2 --warmup 1
 run bench_c3 400 python3 bench.py --workload c3 --steps 3 --warmup 1
+if [ -n "${BENCH_C5:-}" ]; then run bench_c5 900 python3 bench.py --workload c5 --steps 1 --warmup 1; fi
 for w in ${PROFILE_WORKLOADS:-c2 c4 c3}; do
   B="bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline"
   run trace_$w 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$w -o run -- python3 $B
