@@ -8,8 +8,9 @@
 // per-lane stack (rt_kernel.hip).
 //
 // Layout choices (DESIGN.md "Data layout in HBM"):
-//  - a BVH node is one 64-B record (AABB + both child refs): a traversal step
-//    of one lane is one 64-B line, i.e. 4 dwordx4 loads, never six scattered
+//  - a BVH node is one record holding what is needed to test every child
+//    (DNode4: four f32 boxes component-major + four refs, 112 B = 7 dwordx4
+//    loads): one traversal step of a lane reads one record, never scattered
 //    SoA streams (rays are incoherent after the first bounce);
 //  - hot geometry is split from cold attributes: spheres are a double4
 //    {center, radius} stream with materials in a separate int stream (read
