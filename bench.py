@@ -261,7 +261,7 @@ def main():
                             "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
                 "frame_samples": frame_samples,
                 "parallelism": f"row-shard x{world_size}",
-                "bvh": "reference topology" if args.reference_bvh else "binned SAH, two-box f32 nodes",
+                "bvh": "reference topology" if args.reference_bvh else "binned SAH collapsed to 4-wide f32 nodes",
             },
             "roofline": {
                 "bound": "valu-fp64",
