@@ -34,6 +34,9 @@ namespace rtk {
 #define RT_BVH4 1
 #endif
 #define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
+#ifndef RT_RARE_KINDS_UNIFORM
+#define RT_RARE_KINDS_UNIFORM 1
+#endif
 // Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
@@ -50,6 +53,7 @@ struct Diag {
 #ifdef RT_DIAG
     unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0;
     unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
+    unsigned long long load_cyc = 0, loads = 0;  // -DRT_DIAG_LOADLAT: node-load latency (first active lane)
 #endif
 };
 #ifdef RT_DIAG
@@ -1034,9 +1038,19 @@ __device__ __forceinline__ bool trace_filtered_step(const SceneView& S, const Ra
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
                                            float tmin_f, float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq,
-                                           uint32_t& pn) {
+                                           uint32_t& pn, Diag& dg) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
+#ifdef RT_DIAG_LOADLAT
+    const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+#endif
     const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], rq = np[6];
+#ifdef RT_DIAG_LOADLAT
+    __builtin_amdgcn_s_waitcnt(0);
+    if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) {
+        dg.load_cyc += __builtin_amdgcn_s_memtime() - tl0;
+        ++dg.loads;
+    }
+#endif
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
@@ -1144,9 +1158,29 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
         const uint32_t cur = T.cur;
         T.cur = REF_NONE;
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+#if RT_RARE_KINDS_UNIFORM
+        // lists and standalone spheres are rare (none in C2): one wave-uniform
+        // test skips their code, instead of a divergent switch every round
+        if (__ballot(kind != K_BVH && kind != K_NONE)) {
+            if (kind == K_LIST) {
+                const uint32_t child = S.list_children[idx];
+                if (child != REF_NONE) {
+                    if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
+                    T.cur = child;
+                }
+            } else if (kind == K_SPHERE) {
+                pq[pn * RT_BLOCK] = idx;
+                ++pn;
+            }
+        }
         if (kind == K_BVH) {
             RT_DIAG_ONLY(++dg.node_visits;)
-            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
+            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn, dg);
+        }
+#else
+        if (kind == K_BVH) {
+            RT_DIAG_ONLY(++dg.node_visits;)
+            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn, dg);
         } else if (kind == K_LIST) {
             const uint32_t child = S.list_children[idx];
             if (child != REF_NONE) {
@@ -1157,6 +1191,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
             pq[pn * RT_BLOCK] = idx;
             ++pn;
         }
+#endif
     }
     const bool walk = T.cur != REF_NONE || T.sp > 0;
     const unsigned long long mw = __ballot(walk && pn <= ROOM);
@@ -1794,6 +1829,8 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
     atomicAdd(&g_diag[6], dg.node_visits);
     atomicAdd(&g_diag[7], dg.sphere_tests);
     atomicAdd(&g_diag[8], (unsigned long long)n_rays);
+    atomicAdd(&g_diag[9], dg.load_cyc);
+    atomicAdd(&g_diag[10], dg.loads);
 #endif
     atomicAdd(&P->stats[0], (unsigned long long)n_rays);
     if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
