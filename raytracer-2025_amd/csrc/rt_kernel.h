@@ -44,8 +44,6 @@ struct rtk_frame_desc {
 
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" uint32_t rtk_stack_entries(int tier);
-// 1 if the tier's kernel expects sphere child slots as f32 filter records (rth::nodes_sphere_f32)
-extern "C" int rtk_node_sphere_f32(int tier);
 // 1 if the basic tier's kernel walks 4-wide BVH nodes (rth::bvh4_basic)
 extern "C" int rtk_basic_bvh4(void);
 // 1 if the mesh tier's kernel walks 4-wide BVH nodes with every child boxed

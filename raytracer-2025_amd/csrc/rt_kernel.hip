@@ -21,15 +21,13 @@
 
 #include "rt_kernel.h"
 #include "rt_math.h"
+#include "rt_sphere_filter.h"
 
 namespace rtk {
 
-// Basic tier: f32 sphere filter + queued exact f64 sphere tests (sphere_filter); 0 = inline f64 tests.
-#ifndef RT_SPHERE_FILTER
-#define RT_SPHERE_FILTER 0
-#endif
-// Basic tier: 4-wide BVH nodes (rth::bvh4_basic), sphere children through the
-// filter into a per-lane LDS queue of exact tests (visit4); implies the filter.
+// Basic tier: 4-wide BVH nodes (rth::bvh4_convert), sphere children through
+// the f32 filter (rt_sphere_filter.h) into a per-lane LDS queue of exact tests
+// (visit4); 0 = two-box nodes with inline f64 sphere tests.
 #ifndef RT_BVH4
 #define RT_BVH4 1
 #endif
@@ -208,31 +206,6 @@ __device__ __forceinline__ RayF make_rayf(const Ray& r) {
     }
     return R;
 }
-// Per-ray f32 data of the basic tier's sphere filter (sphere_filter below).
-struct SphF {
-    float o[3], d[3];
-    float a;    // |d|^2
-    float gr;   // |o|_1 rounded up
-    float ka;   // 2^-17 a: discriminant error bound per G^2
-    float ehd;  // 2^-19 |d|: error bound of h per G
-    float ia;   // 1/a rounded up (with margin)
-};
-__device__ __forceinline__ SphF make_sphf(const Ray& r) {
-    SphF F;
-    F.o[0] = (float)r.o.x;
-    F.o[1] = (float)r.o.y;
-    F.o[2] = (float)r.o.z;
-    F.d[0] = (float)r.d.x;
-    F.d[1] = (float)r.d.y;
-    F.d[2] = (float)r.d.z;
-    F.a = fmaf(F.d[2], F.d[2], fmaf(F.d[1], F.d[1], F.d[0] * F.d[0]));
-    F.gr = (fabsf(F.o[0]) + fabsf(F.o[1]) + fabsf(F.o[2])) * (1.0f + 0x1p-20f);
-    F.ka = F.a * 0x1p-17f;
-    F.ehd = sqrtf(F.a) * 0x1p-19f;
-    F.ia = (1.0f / F.a) * (1.0f + 0x1p-19f);
-    return F;
-}
-
 __device__ __forceinline__ bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f,
                                        float& entry) {
     const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
@@ -334,7 +307,6 @@ __device__ __forceinline__ Ray xf_ray(const DXform& X, const Ray& r) {
     return Ray{lo, lt - lo, r.time};
 }
 
-constexpr int MAX_XF = 2;
 // The Transforms entered on the way to a hit, innermost last.  Two named
 // fields, not an array: a dynamically indexed private array is placed in
 // scratch memory by the compiler.
@@ -454,66 +426,6 @@ __device__ __forceinline__ uint32_t visit_node(const SceneView& S, uint32_t idx,
         return first0 ? c0 : c1;
     }
     return h0 ? c0 : (h1 ? c1 : REF_NONE);
-}
-
-#ifndef RT_BRANCHLESS
-#define RT_BRANCHLESS 0
-#endif
-// sphere.rs:77-108 with selects instead of branches: both roots, the first
-// accepted one (same result as sphere_t_inv).
-__device__ __forceinline__ bool sphere_t_sel(D3 c, double radius, const Ray& r, double a, double inva, double tmin,
-                                             double tmax, double& t) {
-    const D3 oc = c - r.o;
-    const double h = dot(r.d, oc);
-    const double cc = len2(oc) - radius * radius;
-    const double disc = h * h - a * cc;
-    const double sq = sqrt(fmax(disc, 0.0));
-    const double r1 = div_a(h - sq, a, inva), r2 = div_a(h + sq, a, inva);
-    const bool ok1 = r1 >= tmin && r1 <= tmax, ok2 = r2 >= tmin && r2 <= tmax;
-    t = ok1 ? r1 : r2;
-    return disc >= 0.0 && (ok1 || ok2);
-}
-
-// visit_node for a wave whose lanes diverge between sphere and box children:
-// every lane computes both children's sphere tests (skipped only when no lane
-// of the wave has a sphere child) and both slab tests, and keeps its results
-// with selects -- the work of the union of the two paths, which the wave pays
-// anyway, without the exec-mask bookkeeping of nested divergent branches.
-template <class Stack>
-__device__ __forceinline__ uint32_t visit_node_sel(const SceneView& S, uint32_t idx, const Ray& r, const RayF& rf,
-                                                   double a, double inva, double tmin, float tmin_f, Closest& cl,
-                                                   bool& found, HitInfo& hit, Stack& stk, uint32_t& sp) {
-    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
-    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
-    const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
-    const bool s0 = ref_kind(c0) == K_SPHERE, s1 = ref_kind(c1) == K_SPHERE;
-    if (__ballot(s0 || s1)) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t ch = k ? c1 : c0;
-            const float4 qa = k ? q2 : q0, qb = k ? q3 : q1;
-            const double cx = __hiloint2double(__float_as_int(qa.y), __float_as_int(qa.x));
-            const double cy = __hiloint2double(__float_as_int(qa.w), __float_as_int(qa.z));
-            const double cz = __hiloint2double(__float_as_int(qb.y), __float_as_int(qb.x));
-            const double rr = __hiloint2double(__float_as_int(qb.w), __float_as_int(qb.z));
-            double t;
-            const bool h = sphere_t_sel(d3(cx, cy, cz), rr, r, a, inva, tmin, cl.c, t) && (k ? s1 : s0);
-            const float f = (float)t;
-            cl.c = h ? t : cl.c;
-            cl.c_f = h ? fmaf(fabsf(f), 1.1920928955078125e-07f, f) : cl.c_f;
-            found = found || h;
-            hit.t = h ? t : hit.t;
-            hit.ref = h ? ch : hit.ref;
-        }
-    }
-    float e0, e1;
-    const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
-    const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
-    const bool h0 = slab_f(lo0, hi0, rf, tmin_f, cl.c_f, e0) && c0 != REF_NONE && !s0;
-    const bool h1 = slab_f(lo1, hi1, rf, tmin_f, cl.c_f, e1) && c1 != REF_NONE && !s1;
-    const bool first0 = e0 <= e1;
-    if (h0 && h1) stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
-    return (h0 && (first0 || !h1)) ? c0 : (h1 ? c1 : REF_NONE);
 }
 
 // Pops until an entry whose box can still hold a hit closer than c.
@@ -654,57 +566,6 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
     return t <= tmax;
 }
 
-// sphere_filter for lanes that may hold no sphere (is_sph false): same
-// decisions, taken with selects.
-__device__ __forceinline__ bool sphere_filter_sel(const float4 qa, const float4 qb, const SphF& F, float& c_f,
-                                                  bool is_sph) {
-    const float ocx = qa.x - F.o[0], ocy = qa.y - F.o[1], ocz = qa.z - F.o[2];
-    const float r = qa.w;
-    const float h = fmaf(F.d[2], ocz, fmaf(F.d[1], ocy, F.d[0] * ocx));
-    const float q = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx));
-    const float cc = fmaf(-r, r, q);
-    const float disc = fmaf(h, h, -(F.a * cc));
-    const float G = qb.x + F.gr, G2 = G * G;
-    const float m = F.ka * G2;
-    const float eh = F.ehd * G;
-    const float hh = h + eh;
-    const float clo = fmaf(-0x1p-19f, G2, cc);
-    const bool outside = clo > 0.0f;
-    const bool miss = disc < -m || (outside && (hh < 0.0f || clo > 2.0004f * hh * c_f));
-    const bool sure = outside && disc > m && h > eh && clo > 2.1e-8f * hh;
-    c_f = (is_sph && !miss && sure) ? fminf(c_f, hh * F.ia) : c_f;
-    return is_sph && !miss;
-}
-
-// Up to 4 queued sphere indices, oldest first, in named registers.
-struct Pending {
-    uint32_t n = 0, q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-    // selects, not branches: a branch chain is re-formed into an indexed
-    // private array, which the compiler places in scratch memory
-    __device__ __forceinline__ void push(uint32_t v) {
-        q0 = n == 0 ? v : q0;
-        q1 = n == 1 ? v : q1;
-        q2 = n == 2 ? v : q2;
-        q3 = n == 3 ? v : q3;
-        ++n;
-    }
-    __device__ __forceinline__ void push_if(bool c, uint32_t v) {
-        q0 = (c && n == 0) ? v : q0;
-        q1 = (c && n == 1) ? v : q1;
-        q2 = (c && n == 2) ? v : q2;
-        q3 = (c && n == 3) ? v : q3;
-        n += c ? 1u : 0u;
-    }
-    __device__ __forceinline__ uint32_t pop() {
-        const uint32_t v = q0;
-        q0 = q1;
-        q1 = q2;
-        q2 = q3;
-        --n;
-        return v;
-    }
-};
-
 // world.hit(r, [1e-8, inf)) (camera.rs:286) as a depth-first walk with one
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
@@ -724,8 +585,8 @@ struct Trav {
     bool found;
     HitInfo hit;
     uint32_t nmed;  // FULL: media met by the walk, tested after it (media_phase)
-    SphF sf;        // BASIC with the sphere filter: per-ray f32 data
-    Pending pd;     // and the spheres queued for the exact test
+    SphF sf;        // BASIC (4-wide): the sphere filter's per-ray f32 data
+    uint32_t pn;    // and the number of spheres queued for the exact test
 };
 
 template <int TIER>
@@ -742,9 +603,10 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     T.found = false;
     T.hit.nxf = 0;
     T.nmed = 0;
-    if constexpr (TIER == TIER_BASIC && (RT_SPHERE_FILTER || RT_BVH4)) {
-        T.sf = make_sphf(wr);
-        T.pd.n = 0;
+    if constexpr (TIER == TIER_BASIC && RT_BVH4) {
+        const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
+        T.sf = make_sphf(o, d);
+        T.pn = 0;
     }
 }
 
@@ -786,8 +648,6 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
         if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (TIER == TIER_FULL && RT_FULL_BVH4))
             T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
-        else if constexpr (TIER == TIER_BASIC && RT_BRANCHLESS)
-            T.cur = visit_node_sel(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, T.found, T.hit, stk, T.sp);
         else
             T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
     } else if (kind == K_SPHERE) {
@@ -878,157 +738,10 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, T
     T.nmed = 0;
 }
 
-// ------------------------------------------------------------------ basic tier: f32 sphere filter
-// Inline, a node visit runs the f64 sphere test (sphere.rs:77-108) of every
-// sphere child, and a wave pays for the union of the sphere path and the box
-// path of its lanes -- on C2 almost every visit.  With the filter, a sphere
-// child's slot holds the sphere in f32 (rt_layout.h DNodeSlot::fsph) and the
-// visit runs a conservative f32 test:
-//  - it rejects only spheres the exact test is certain to miss: discriminant
-//    below minus its error bound, the sphere behind an origin outside it, or
-//    its near root beyond the walk's f32 bound of the closest t;
-//  - when the near root is certain to be accepted, its upper bound h/a
-//    (closest approach, >= the near root) lowers that bound at once, so the
-//    walk culls as it did with the exact test;
-//  - every other sphere is queued (idx, up to 4 per lane, in registers) and
-//    tested exactly in f64 in sphere rounds, which the wave runs when enough
-//    lanes have one queued or no lane can walk further.
-// Error bounds (u = 2^-24, G = |c|_1 + r + |o|_1 >= every magnitude involved,
-// inputs rounded to nearest f32): |h - h*| <= 6.2u |d| G, |cc - cc*| <= 10.4u G^2,
-// |disc - disc*| <= 31u a G^2; the kernel uses 32u |d| G, 32u G^2 and 128u a G^2.
-// The reference's own f64 rounding is orders of magnitude below these.  So the
-// closest hit is the one the inline f64 tests find (tests/test_parity_gpu.py).
+// ------------------------------------------------------------------ basic tier: sphere rounds
 #ifndef RT_DEFER_THRESH
 #define RT_DEFER_THRESH 48  // lanes with a queued sphere that trigger a sphere round
 #endif
-#ifndef RT_DEFER_BLOCKED
-#define RT_DEFER_BLOCKED 65  // lanes blocked on a full queue that trigger one (65 = never)
-#endif
-
-// The f32 sphere test of one fsph slot {c, r | g}: false when the exact test
-// is certain not to give a hit closer than c_f; lowers c_f when it is certain
-// to give one.
-__device__ __forceinline__ bool sphere_filter(const float4 qa, const float4 qb, const SphF& F, float& c_f) {
-    const float ocx = qa.x - F.o[0], ocy = qa.y - F.o[1], ocz = qa.z - F.o[2];
-    const float r = qa.w;
-    const float h = fmaf(F.d[2], ocz, fmaf(F.d[1], ocy, F.d[0] * ocx));
-    const float q = fmaf(ocz, ocz, fmaf(ocy, ocy, ocx * ocx));
-    const float cc = fmaf(-r, r, q);
-    const float disc = fmaf(h, h, -(F.a * cc));
-    const float G = qb.x + F.gr, G2 = G * G;
-    const float m = F.ka * G2;
-    const float eh = F.ehd * G;
-    const float hh = h + eh;                        // >= h
-    const float clo = fmaf(-0x1p-19f, G2, cc);      // <= cc
-    const bool outside = clo > 0.0f;                // origin certainly outside: roots of one sign
-    // near root >= cc / 2h > c_f (both roots beyond the bound), or both roots < 0
-    if (disc < -m || (outside && (hh < 0.0f || clo > 2.0004f * hh * c_f))) return false;
-    // near root certainly >= t_min (cc / 2h > 1e-8) and the ray certainly hits: t <= h / a
-    if (outside && disc > m && h > eh && clo > 2.1e-8f * hh) c_f = fminf(c_f, hh * F.ia);
-    return true;
-}
-
-// One node visit with filtered sphere children: box children get the f32
-// slab test and are walked near-first; sphere children the filter (queued).
-template <class Stack>
-__device__ __forceinline__ uint32_t visit_filtered(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
-                                                   float tmin_f, float& c_f, Stack& stk, uint32_t& sp, Pending& pd) {
-    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes + idx);
-    const float4 q0 = np[0], q1 = np[1], q2 = np[2], q3 = np[3], q4 = np[4];
-    const uint32_t c0 = __float_as_uint(q4.x), c1 = __float_as_uint(q4.y);
-    bool h0 = false, h1 = false;
-    float e0 = 0.0f, e1 = 0.0f;
-    if constexpr (RT_BRANCHLESS) {  // both filters and both slab tests on every lane, kept by selects
-        const bool s0 = ref_kind(c0) == K_SPHERE, s1 = ref_kind(c1) == K_SPHERE;
-        if (__ballot(s0 || s1)) {
-            const bool k0 = sphere_filter_sel(q0, q1, sf, c_f, s0), k1 = sphere_filter_sel(q2, q3, sf, c_f, s1);
-            pd.push_if(k0, ref_index(c0));
-            pd.push_if(k1, ref_index(c1));
-        }
-        const float lo0[3] = {q0.x, q0.y, q0.z}, hi0[3] = {q0.w, q1.x, q1.y};
-        const float lo1[3] = {q2.x, q2.y, q2.z}, hi1[3] = {q2.w, q3.x, q3.y};
-        h0 = slab_f(lo0, hi0, rf, tmin_f, c_f, e0) && c0 != REF_NONE && !s0;
-        h1 = slab_f(lo1, hi1, rf, tmin_f, c_f, e1) && c1 != REF_NONE && !s1;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const uint32_t ch = k ? c1 : c0;
-            const float4 qa = k ? q2 : q0, qb = k ? q3 : q1;
-            bool& hk = k ? h1 : h0;
-            float& ek = k ? e1 : e0;
-            if (ch == REF_NONE) continue;
-            if (ref_kind(ch) == K_SPHERE) {
-                if (sphere_filter(qa, qb, sf, c_f)) pd.push(ref_index(ch));
-            } else {
-                const float lo[3] = {qa.x, qa.y, qa.z}, hi[3] = {qa.w, qb.x, qb.y};
-                hk = slab_f(lo, hi, rf, tmin_f, c_f, ek);
-            }
-        }
-    }
-    h0 = h0 && e0 <= c_f;
-    h1 = h1 && e1 <= c_f;
-    if (h0 && h1) {
-        const bool first0 = e0 <= e1;
-        stk.push(sp++, first0 ? c1 : c0, first0 ? e1 : e0);
-        return first0 ? c0 : c1;
-    }
-    return h0 ? c0 : (h1 ? c1 : REF_NONE);
-}
-
-// world.hit for the basic tier (spheres, lists, BVHs) with the sphere filter,
-// one wave iteration per call: lanes that can walk visit one node (f32 only);
-// then, when enough lanes have a sphere queued (or none walks any more), each
-// of those tests one exactly in f64 (sphere.rs:77-108).  A lane whose queue is
-// full waits for that before walking on.  Returns false when the lane's walk
-// and queue are both done; same closest hit as trace_step's walk.
-template <class Stack>
-__device__ __forceinline__ bool trace_filtered_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
-                                                    Diag& dg) {
-    constexpr double tmin = 1e-8;
-    const float tmin_f = f32_down(tmin);
-    RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
-    if ((T.cur != REF_NONE || T.sp > 0) && T.pd.n <= 2) {  // node round
-        RT_DIAG_ONLY(++dg.lane_trace_iters;)
-        if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
-        const uint32_t cur = T.cur;
-        T.cur = REF_NONE;
-        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
-        if (kind == K_BVH) {
-            RT_DIAG_ONLY(++dg.node_visits;)
-            T.cur = visit_filtered(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, T.pd);
-        } else if (kind == K_LIST) {
-            const uint32_t child = S.list_children[idx];
-            if (child != REF_NONE) {
-                if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                T.cur = child;
-            }
-        } else if (kind == K_SPHERE) {
-            T.pd.push(idx);
-        }
-    }
-    const bool walk = T.cur != REF_NONE || T.sp > 0;
-    // lanes that can walk on without a sphere round: when there are none, the
-    // round runs whatever the count (a lane blocked on a full queue counts as
-    // not walking, else it would wait on itself)
-    const unsigned long long mw = __ballot(walk && T.pd.n <= 2);
-    const unsigned long long mp = __ballot(T.pd.n > 0);
-    const unsigned long long mb = __ballot(walk && T.pd.n > 2);
-    if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH || __popcll(mb) >= RT_DEFER_BLOCKED) {
-        if (T.pd.n > 0) {  // sphere round
-            RT_DIAG_ONLY(++dg.sphere_tests;)
-            const uint32_t idx = T.pd.pop();
-            const double4 s4 = S.spheres[idx];
-            double t;
-            if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
-                T.cl.lower(t);
-                T.found = true;
-                T.hit.t = t;
-                T.hit.ref = make_ref(K_SPHERE, idx);
-            }
-        }
-    }
-    return walk || T.pd.n > 0;
-}
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
@@ -1060,8 +773,7 @@ __device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, con
     if (__ballot(sph[0] || sph[1] || sph[2] || sph[3])) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            if (sphere_filter_sel(make_float4(LX[i], LY[i], LZ[i], HX[i]), make_float4(HY[i], 0.0f, 0.0f, 0.0f), sf,
-                                  c_f, sph[i])) {
+            if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
                 pq[pn * RT_BLOCK] = ref_index(R[i]);
                 ++pn;
             }
@@ -1141,9 +853,13 @@ __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t id
     return key[0] < INF ? ref[0] : REF_NONE;
 }
 
-// world.hit for the basic tier over 4-wide nodes, one wave iteration per call
-// (as trace_filtered_step): a node round for lanes with room in their queue,
-// then a sphere round when enough lanes have a test queued or none can walk.
+// world.hit for the basic tier over 4-wide nodes, one wave iteration per call:
+// a node round (f32 only) for lanes with room in their queue, then a sphere
+// round -- each lane with a queued sphere tests one exactly in f64
+// (sphere.rs:77-108) -- when 48 lanes have one queued or none can walk on.  A
+// lane whose queue is full waits for that before walking on.  Returns false
+// when the lane's walk and queue are both done; same closest hit as
+// trace_step's walk (A/B renders: RMSE 0).
 template <class Stack>
 __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
                                             uint32_t* pq, Diag& dg) {
@@ -1151,7 +867,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const float tmin_f = f32_down(tmin);
     constexpr uint32_t ROOM = RT_PEND_CAP - 4;  // a visit queues at most 4
     RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
-    uint32_t pn = T.pd.n;
+    uint32_t pn = T.pn;
     if ((T.cur != REF_NONE || T.sp > 0) && pn <= ROOM) {  // node round
         RT_DIAG_ONLY(++dg.lane_trace_iters;)
         if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
@@ -1211,7 +927,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
             }
         }
     }
-    T.pd.n = pn;
+    T.pn = pn;
     return walk || pn > 0;
 }
 
@@ -1765,8 +1481,6 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
         auto step = [&]() -> bool {
             if constexpr (TIER == TIER_BASIC && RT_BVH4) {
                 return trace4_step(S, ray, T, stk, pq, dg);
-            } else if constexpr (TIER == TIER_BASIC && RT_SPHERE_FILTER) {
-                return trace_filtered_step(S, ray, T, stk, dg);
             } else {
                 RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
                 return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
@@ -1933,7 +1647,6 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     return rtk::TIER_BASIC;
 }
 
-extern "C" int rtk_node_sphere_f32(int tier) { return tier == rtk::TIER_BASIC && RT_SPHERE_FILTER && !RT_BVH4; }
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }
 extern "C" int rtk_full_bvh4(void) { return RT_FULL_BVH4; }

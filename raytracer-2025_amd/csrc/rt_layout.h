@@ -59,10 +59,6 @@ constexpr uint32_t REF_NONE = 0u;
 //    the slab test is made conservative (rt_kernel.hip slab_f), so every hit
 //    the reference's exact-box f64 test admits is admitted.
 // c1 may be REF_NONE (a BVH over one object, bvh.rs:25).
-// Basic tier with the f32 sphere filter (rt_kernel.hip sphere_filter): a sphere
-// child's slot holds the sphere rounded to nearest f32 plus g = |c|_1 + r
-// rounded up, the magnitude the filter's error bounds scale with; the exact
-// f64 sphere is read from `spheres` when the filter cannot decide.
 struct alignas(16) DNodeSlot {
     union {
         struct {
@@ -70,11 +66,6 @@ struct alignas(16) DNodeSlot {
             uint32_t pad[2];
         } box;
         double sphere[4];  // {cx, cy, cz, r}
-        struct {
-            float c[3], r;
-            float g;
-            uint32_t pad[3];
-        } fsph;
     };
 };
 struct alignas(16) DNode {
@@ -87,7 +78,8 @@ static_assert(sizeof(DNode) == 80, "DNode must be 80 B (5 dwordx4)");
 // Basic-tier 4-wide BVH node (rth::bvh4_basic): up to four children, their
 // f32 boxes (rounded outward) stored component-major so one dwordx4 holds one
 // bound of all four.  A sphere child keeps the sphere filter's record in its
-// box slots instead: lo = center, hi.x = radius, hi.y = g (as DNodeSlot::fsph).
+// box slots instead: lo = center, hi.x = radius, hi.y = g = |c|_1 + r rounded
+// up (rt_sphere_filter.h), all rounded to nearest but g.
 struct alignas(16) DNode4 {
     float lo[3][4], hi[3][4];
     uint32_t ref[4];  // REF_NONE for an unused slot

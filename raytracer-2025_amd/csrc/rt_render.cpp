@@ -79,7 +79,6 @@ static int prepare_tier(HostWorld& hw) {
             return -1;
         }
     }
-    if (rtk_node_sphere_f32(tier)) nodes_sphere_f32(hw);
     return tier;
 }
 

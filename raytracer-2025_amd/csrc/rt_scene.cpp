@@ -1054,25 +1054,6 @@ void rt_scene_destroy(rt_scene* s) {
 }  // extern "C"
 
 namespace rth {
-void nodes_sphere_f32(HostWorld& hw) {
-    for (rtk::DNode& n : hw.nodes) {
-        const uint32_t refs[2] = {n.c0, n.c1};
-        for (int k = 0; k < 2; ++k) {
-            if (rtk::ref_kind(refs[k]) != rtk::K_SPHERE) continue;
-            const double c[3] = {n.slot[k].sphere[0], n.slot[k].sphere[1], n.slot[k].sphere[2]};
-            const double r = n.slot[k].sphere[3];
-            auto& fs = n.slot[k].fsph;
-            double g = 0.0;
-            for (int a = 0; a < 3; ++a) {
-                fs.c[a] = (float)c[a];
-                g += std::fabs((double)fs.c[a]);
-            }
-            fs.r = (float)r;
-            fs.g = round_up(g + std::fabs((double)fs.r));
-            fs.pad[0] = fs.pad[1] = fs.pad[2] = 0;
-        }
-    }
-}
 }  // namespace rth
 
 namespace rth {

@@ -155,11 +155,6 @@ int32_t set_error(int32_t code, const std::string& msg);
 // the binned-SAH rebuild (closest-hit results agree up to exact t ties).
 int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t background_tex, bool reference_bvh,
                 HostWorld& out);
-// Rewrites every sphere child slot of every BVH node as the f32 record of the
-// basic tier's sphere filter (DNodeSlot::fsph: center and radius rounded to
-// nearest, g = |c|_1 + r rounded up): the node format of kernels that test
-// spheres in f32 first and queue the exact f64 test (rtk_node_sphere_f32).
-void nodes_sphere_f32(HostWorld& hw);
 // Collapses every two-box BVH into 4-wide nodes (hw.nodes4; sphere children as
 // filter records when filter_spheres, the basic tier), rewrites the K_BVH refs
 // to index nodes4 and recomputes stack_need.  Returns the new stack_need (hw is
