@@ -21,6 +21,7 @@
 
 #include "rt_kernel.h"
 #include "rt_math.h"
+#include "rt_slab.h"
 #include "rt_sphere_filter.h"
 
 namespace rtk {
@@ -176,46 +177,9 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
 }
 
 // ------------------------------------------------------------------ geometry tests
-// aabb.rs:62-78 slab test, in f32, made conservative: whenever the
-// reference's f64 test on the exact box admits [tmin, c], this one does too.
-//  - boxes are stored rounded outward (flatten);
-//  - the origin's f32 rounding (and the rounding of o*idf) is absorbed by
-//    widening the slab by pad = 2^-22 |o| per axis in space (RayF::nlo/nhi);
-//  - the fma and 1/d roundings (relative, < 3u) by widening the t-interval
-//    by 2^-22 |t| (REL);
-//  - 1/d is clamped to |.| <= 2^60 so a zero direction component gives huge
-//    finite t (the reference's +-inf) instead of inf - inf = NaN.
-struct RayF {
-    float idf[3];  // 1/d
-    float nlo[3];  // -(o + pad) * idf  (lo planes moved outward)
-    float nhi[3];  // -(o - pad) * idf  (hi planes moved outward)
-};
 __device__ __forceinline__ RayF make_rayf(const Ray& r) {
-    RayF R;
     const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double id = 1.0 / d[k];
-        float f = (float)id;
-        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, (float)id);
-        const float of = (float)o[k];
-        const float pad = fabsf(of) * 2.384185791015625e-07f + 1e-30f;
-        R.idf[k] = f;
-        R.nlo[k] = -((of + pad) * f);
-        R.nhi[k] = -((of - pad) * f);
-    }
-    return R;
-}
-__device__ __forceinline__ bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f,
-                                       float& entry) {
-    const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
-    const float tly = fmaf(lo[1], R.idf[1], R.nlo[1]), thy = fmaf(hi[1], R.idf[1], R.nhi[1]);
-    const float tlz = fmaf(lo[2], R.idf[2], R.nlo[2]), thz = fmaf(hi[2], R.idf[2], R.nhi[2]);
-    const float nr = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
-    const float fr = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
-    constexpr float REL = 2.384185791015625e-07f;  // 2^-22
-    entry = fmaxf(fmaf(-fabsf(nr), REL, nr), tmin_f);
-    return entry <= fminf(fmaf(fabsf(fr), REL, fr), c_f);
+    return make_rayf(o, d);
 }
 
 // sphere.rs:77-96 -- t of the accepted root, or false
@@ -354,14 +318,6 @@ struct StackT {
 template <int TIER>
 using StackFor = StackT<tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
                         TIER != TIER_BASIC>;
-__device__ __forceinline__ float f32_down(double x) {
-    float f = (float)x;  // round-to-nearest; step one ulp down when it rounded up
-    if ((double)f > x) {
-        const uint32_t b = __float_as_uint(f);
-        f = (f > 0.0f) ? __uint_as_float(b - 1u) : (f == 0.0f ? -1.401298464e-45f : __uint_as_float(b + 1u));
-    }
-    return f;
-}
 
 // Closest-hit state of one traversal: t and its f32 upper bound.
 struct Closest {

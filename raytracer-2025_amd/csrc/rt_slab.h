@@ -1,0 +1,79 @@
+// rt_slab.h -- the conservative f32 box test every kernel tier walks with.
+//
+// Host and device: the kernel (rt_kernel.hip) runs it, and the CPU property
+// test (tests/test_slab_cpu.py, tests/cpp/slab_prop.cpp) checks it against the
+// slab test of aabb.rs:62-78 evaluated in extended precision.
+//
+// aabb.rs:62-78: per axis t0 = (lo - o) / d, t1 = (hi - o) / d, the interval
+// [min, max] of the two intersected with the ray's [t_min, t_max]; a hit when
+// the result is not empty (inclusive).  Here in f32, made conservative --
+// whenever the exact test on the exact box admits part of [t_min, c], this one
+// does too:
+//  - boxes are stored rounded outward (rth flatten / bvh4_convert);
+//  - the origin's f32 rounding (and the rounding of o * idf) is absorbed by
+//    widening the slab by pad = 2^-22 |o| per axis in space (RayF::nlo/nhi);
+//  - the fma and 1/d roundings (relative, < 3u) by widening the t-interval
+//    by 2^-22 |t| (REL);
+//  - 1/d is clamped to |.| <= 2^60 so a zero direction component gives huge
+//    finite t (the reference's +-inf) instead of inf - inf = NaN.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#define RT_HD inline
+#endif
+
+namespace rtk {
+
+struct RayF {
+    float idf[3];  // 1/d
+    float nlo[3];  // -(o + pad) * idf  (lo planes moved outward)
+    float nhi[3];  // -(o - pad) * idf  (hi planes moved outward)
+};
+
+RT_HD RayF make_rayf(const double o[3], const double d[3]) {
+    RayF R;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double id = 1.0 / d[k];
+        float f = (float)id;
+        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, (float)id);
+        const float of = (float)o[k];
+        const float pad = fabsf(of) * 2.384185791015625e-07f + 1e-30f;
+        R.idf[k] = f;
+        R.nlo[k] = -((of + pad) * f);
+        R.nhi[k] = -((of - pad) * f);
+    }
+    return R;
+}
+
+// f32 not above x (round to nearest, then one ulp down when that rounded up)
+RT_HD float f32_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) {
+        union {
+            float f;
+            uint32_t u;
+        } b{f};
+        b.u = (f > 0.0f) ? b.u - 1u : (f == 0.0f ? 0x80000001u : b.u + 1u);
+        f = b.f;
+    }
+    return f;
+}
+
+// Entry distance (clamped to t_min) and hit of box [lo, hi] for t in [tmin_f, c_f].
+RT_HD bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f, float& entry) {
+    const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
+    const float tly = fmaf(lo[1], R.idf[1], R.nlo[1]), thy = fmaf(hi[1], R.idf[1], R.nhi[1]);
+    const float tlz = fmaf(lo[2], R.idf[2], R.nlo[2]), thz = fmaf(hi[2], R.idf[2], R.nhi[2]);
+    const float nr = fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz));
+    const float fr = fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz));
+    constexpr float REL = 2.384185791015625e-07f;  // 2^-22
+    entry = fmaxf(fmaf(-fabsf(nr), REL, nr), tmin_f);
+    return entry <= fminf(fmaf(fabsf(fr), REL, fr), c_f);
+}
+
+}  // namespace rtk

@@ -1,0 +1,32 @@
+"""The kernels' conservative f32 box test (raytracer-2025_amd/csrc/rt_slab.h,
+the same source the gfx950 kernel compiles) against the slab test of
+aabb.rs:62-78 evaluated in long double on the exact box: every box hit the
+exact test admits within [t_min, c] must be admitted by the f32 test on the box
+rounded outward (tests/cpp/slab_prop.cpp) -- the property that makes the f32
+walk's closest hits the f64 reference's.  Random and adversarial cases:
+origins on faces, edges, corners and inside, rays aimed at boundary points,
+zero direction components, flat boxes, boxes 1e4 away, box sizes over seven
+decades, c at the entry distance.  Built with and without FMA contraction."""
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+
+@pytest.mark.parametrize("contract", ["fast", "off"])
+@pytest.mark.parametrize("seed", [2025, 7])
+def test_slab_is_conservative(contract, seed):
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "slab_prop_" + contract)
+    flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
+    subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "slab_prop.cpp"), "-o", exe],
+                   check=True)
+    r = subprocess.run([exe, "1500000", str(seed)], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-2000:])
+    assert r.returncode == 0, r.stdout[-3000:]
+    n, hits, fhits, bad = map(int, r.stdout.strip().split("\n")[-1].split())
+    assert bad == 0
+    assert hits > n // 5 and fhits >= hits
