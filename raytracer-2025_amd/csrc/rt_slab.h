@@ -28,6 +28,43 @@
 
 namespace rtk {
 
+#ifndef RT_SLAB_FOLD
+#define RT_SLAB_FOLD 1
+#endif
+
+#if RT_SLAB_FOLD
+// The t-interval widening folded into the ray: the plane distances of the
+// near planes (lo when 1/d > 0) are scaled by 1 - 2^-21, those of the far
+// planes by 1 + 2^-21, so the box's entry is moved earlier and its exit later
+// by that relative amount whenever they are positive -- the only case where
+// they decide a hit (a negative entry is clamped to t_min, a negative exit
+// misses either way).  The scalings' own roundings are covered by the doubled
+// widths: pad = 2^-21 |o| in space, 2^-21 relative in t.
+struct RayF {
+    float idl[3], idh[3];  // 1/d scaled for the lo and hi planes
+    float nlo[3];          // -(o + pad) * idl  (lo planes moved outward)
+    float nhi[3];          // -(o - pad) * idh  (hi planes moved outward)
+};
+
+RT_HD RayF make_rayf(const double o[3], const double d[3]) {
+    RayF R;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double id = 1.0 / d[k];
+        float f = (float)id;
+        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, (float)id);
+        const float of = (float)o[k];
+        const float pad = fabsf(of) * 4.76837158203125e-07f + 1e-30f;  // 2^-21 |o|
+        constexpr float SHRINK = 1.0f - 4.76837158203125e-07f, GROW = 1.0f + 4.76837158203125e-07f;
+        const float sl = f > 0.0f ? SHRINK : GROW, sh = f > 0.0f ? GROW : SHRINK;
+        R.idl[k] = f * sl;
+        R.idh[k] = f * sh;
+        R.nlo[k] = -((of + pad) * f) * sl;
+        R.nhi[k] = -((of - pad) * f) * sh;
+    }
+    return R;
+}
+#else
 struct RayF {
     float idf[3];  // 1/d
     float nlo[3];  // -(o + pad) * idf  (lo planes moved outward)
@@ -49,6 +86,7 @@ RT_HD RayF make_rayf(const double o[3], const double d[3]) {
     }
     return R;
 }
+#endif
 
 // f32 not above x (round to nearest, then one ulp down when that rounded up)
 RT_HD float f32_down(double x) {
@@ -66,6 +104,13 @@ RT_HD float f32_down(double x) {
 
 // Entry distance (clamped to t_min) and hit of box [lo, hi] for t in [tmin_f, c_f].
 RT_HD bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f, float c_f, float& entry) {
+#if RT_SLAB_FOLD
+    const float tlx = fmaf(lo[0], R.idl[0], R.nlo[0]), thx = fmaf(hi[0], R.idh[0], R.nhi[0]);
+    const float tly = fmaf(lo[1], R.idl[1], R.nlo[1]), thy = fmaf(hi[1], R.idh[1], R.nhi[1]);
+    const float tlz = fmaf(lo[2], R.idl[2], R.nlo[2]), thz = fmaf(hi[2], R.idh[2], R.nhi[2]);
+    entry = fmaxf(fmaxf(fmaxf(fminf(tlx, thx), fminf(tly, thy)), fminf(tlz, thz)), tmin_f);
+    return entry <= fminf(fminf(fminf(fmaxf(tlx, thx), fmaxf(tly, thy)), fmaxf(tlz, thz)), c_f);
+#else
     const float tlx = fmaf(lo[0], R.idf[0], R.nlo[0]), thx = fmaf(hi[0], R.idf[0], R.nhi[0]);
     const float tly = fmaf(lo[1], R.idf[1], R.nlo[1]), thy = fmaf(hi[1], R.idf[1], R.nhi[1]);
     const float tlz = fmaf(lo[2], R.idf[2], R.nlo[2]), thz = fmaf(hi[2], R.idf[2], R.nhi[2]);
@@ -74,6 +119,7 @@ RT_HD bool slab_f(const float* lo, const float* hi, const RayF& R, float tmin_f,
     constexpr float REL = 2.384185791015625e-07f;  // 2^-22
     entry = fmaxf(fmaf(-fabsf(nr), REL, nr), tmin_f);
     return entry <= fminf(fmaf(fabsf(fr), REL, fr), c_f);
+#endif
 }
 
 }  // namespace rtk

@@ -57,10 +57,12 @@ int main(int argc, char** argv) {
             lo[k] = c - w;
             hi[k] = c + w;
         }
-        // origin: outside, on a face, on an edge or corner, or inside
-        const int ok = (int)(U(rng) * 4);
+        // origin: outside, on a face, on an edge or corner, inside, or remote
+        // (a camera near the world origin, the box up to 1e4 away)
+        const int ok = (int)(U(rng) * 5);
         for (int k = 0; k < 3; ++k) {
             if (ok == 0) o[k] = lo[k] + (hi[k] - lo[k]) * (3 * U(rng) - 1) + (U(rng) - 0.5) * 10 * scale;
+            else if (ok == 4) o[k] = 20 * (U(rng) - 0.5);
             else if (ok == 2) o[k] = U(rng) < 0.5 ? lo[k] : hi[k];
             else o[k] = lo[k] + (hi[k] - lo[k]) * U(rng);
         }
@@ -72,9 +74,13 @@ int main(int argc, char** argv) {
         // grazing along a face; zero components sometimes
         const int dk = (int)(U(rng) * 3);
         if (dk == 0) {
+            // a boundary point nudged by 1e-11 .. 1e-5 of the box size, so
+            // the exact gap is where f32 rounding decides
+            const double nudge = std::exp(std::log(1e-11) + U(rng) * std::log(1e6)) * (U(rng) - 0.5) * (scale + 1e-3);
             for (int k = 0; k < 3; ++k) {
                 const double u = U(rng);
-                const double p = U(rng) < 0.3 ? (u < 0.5 ? lo[k] : hi[k]) : lo[k] + (hi[k] - lo[k]) * u;
+                const double p = U(rng) < 0.5 ? (u < 0.5 ? lo[k] : hi[k]) + nudge * (U(rng) - 0.5)
+                                              : lo[k] + (hi[k] - lo[k]) * u;
                 d[k] = p - o[k];
             }
         } else {
