@@ -600,7 +600,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
             T.hit.xf = T.xfs;
         }
     };
-    RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE) ++dg.sphere_tests;)
+    RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
     if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
         if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (TIER == TIER_FULL && RT_FULL_BVH4))
             T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);

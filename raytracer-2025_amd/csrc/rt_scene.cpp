@@ -401,6 +401,30 @@ struct Flattener {
                     r = emit(o.children[0], in_boundary, xf_depth);
                     break;
                 }
+                // A list holding BVHs (the C4 / C5 worlds: meshes or sphere
+                // clouds beside a few loose objects) is walked as a BVH over
+                // its elements: Hittables::hit keeps the closest of all its
+                // children (hits.rs:34-46), which any BVH over them finds too
+                // (up to exact t ties, as for every rebuilt BVH) -- without
+                // one walk iteration per element.  Lists of plain primitives
+                // (C3's Cornell box) stay lists: they keep the BVH-free tier.
+                if (!reference_bvh && !no_collapse && o.children.size() >= 2 &&
+                    std::any_of(o.children.begin(), o.children.end(),
+                                [&](int c) { return s->objs[c].kind == O_BVH; })) {
+                    std::vector<Item> items;
+                    for (int c : o.children) {
+                        auto e = emit(c, in_boundary, xf_depth);
+                        Item x;
+                        x.ref = e.first;
+                        x.need = e.second;
+                        x.box = tight(c);
+                        for (int k = 0; k < 3; ++k) x.c[k] = 0.5 * (x.box.a[k].lo + x.box.a[k].hi);
+                        items.push_back(x);
+                    }
+                    out.n_bvh_leaves += items.size();
+                    r = sah(items, 0, items.size());
+                    break;
+                }
                 std::vector<std::pair<uint32_t, uint32_t>> kids;
                 for (int c : o.children) kids.push_back(emit(c, in_boundary, xf_depth));
                 uint32_t start = (uint32_t)out.list_children.size();

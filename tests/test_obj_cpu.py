@@ -100,8 +100,9 @@ def test_usemtl_splits_models_and_unknown_material_is_empty(product, capi, rt, t
     s, w = load(product, rt, write(tmp_path, obj))
     info = prims(product, capi, s, w)
     assert info.primitives == 4
-    # three models -> three BVHs over 2 + 1 + 1 triangles (a 1-object BVH is one node)
-    assert info.bvh_leaves == 4
+    # three models -> three BVHs over 2 + 1 + 1 triangles (a 1-object BVH is one
+    # node), and the list of the three is walked as a BVH over them (+3 leaves)
+    assert info.bvh_leaves == 4 + 3
 
 
 def test_missing_mtl_loads_nothing(product, oracle, capi, rt, tmp_path):
