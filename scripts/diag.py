@@ -53,7 +53,7 @@ out = {
     "trace_iters_per_ray": c[5] / c[8],
     "wave_trace_iters_per_wave_bounce": c[3] / max(1, c[4]),
     "node_visits_per_ray": c[6] / c[8],
-    "queued_f64_sphere_tests_per_ray": c[7] / c[8],
+    "primitive_tests_per_ray": c[7] / c[8],
     "node_load_wave_cycles": c[9] / c[10] if c[10] else None,
     "raw": c[:11],
 }
