@@ -419,6 +419,23 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             cur = pop(stk, sp, sp0, cl.c_f);
             if (cur == REF_NONE) break;
         }
+        uint32_t after = REF_NONE;  // as trace_step: a primitive list element is tested in the list step
+        if (ref_kind(cur) == K_LIST) {
+            const uint32_t li = ref_index(cur);
+            const uint32_t child = S.list_children[li];
+            cur = REF_NONE;
+            if (child == REF_NONE) continue;
+            const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
+            const uint32_t ck = ref_kind(child);
+            if (ck == K_SPHERE || ck == K_QUAD || ck == K_TRI || ck == K_MSPHERE) {
+                cur = child;
+                after = nxt;
+            } else {
+                if (nxt != REF_NONE) stk.push(sp++, nxt, NO_CULL);
+                cur = child;
+                continue;
+            }
+        }
         const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
         cur = REF_NONE;
         double t;
@@ -431,14 +448,6 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 else
                     cur = visit_node(S, idx, r, rf, a, inva, tmin, tmin_f, cl, stk, sp, on_hit);
                 break;
-            case K_LIST: {
-                const uint32_t child = S.list_children[idx];
-                if (child != REF_NONE) {
-                    if (S.list_children[idx + 1] != REF_NONE) stk.push(sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                    cur = child;
-                }
-                break;
-            }
             case K_SPHERE: {
                 const double4 s = S.spheres[idx];
                 if (sphere_t_inv(d3(s.x, s.y, s.z), s.w, r, a, inva, tmin, cl.c, t)) {
@@ -485,6 +494,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             }
             default: break;
         }
+        if (after != REF_NONE) cur = after;
     }
     tbest = cl.c;
     return found;
@@ -586,9 +596,30 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
 #endif
     }
     const Ray& r = FULL ? T.r : wr;
-    const uint32_t kind = ref_kind(T.cur), idx = ref_index(T.cur);
-    const uint32_t this_ref = T.cur;
+    uint32_t cur = T.cur;
     T.cur = REF_NONE;
+    // A list step whose element is a primitive tests it right here and goes
+    // on with the next element (no stack round trip, one step per element);
+    // a compound element (BVH, Transform, medium, list) is walked next with
+    // the rest of the list pushed.
+    uint32_t after = REF_NONE;
+    if (ref_kind(cur) == K_LIST) {
+        const uint32_t li = ref_index(cur);
+        const uint32_t child = S.list_children[li];
+        if (child == REF_NONE) return true;  // empty list
+        const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
+        const uint32_t ck = ref_kind(child);
+        if (ck == K_SPHERE || ck == K_QUAD || ck == K_TRI || (FULL && ck == K_MSPHERE)) {
+            cur = child;
+            after = nxt;
+        } else {
+            if (nxt != REF_NONE) stk.push(T.sp++, nxt, NO_CULL);
+            T.cur = child;
+            return true;
+        }
+    }
+    const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+    const uint32_t this_ref = cur;
     double t;
     bool got = false;
     auto record = [&](uint32_t ref, double tt) {
@@ -609,12 +640,6 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     } else if (kind == K_SPHERE) {
         const double4 sp4 = S.spheres[idx];
         got = sphere_t_inv(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, T.inva, tmin, T.cl.c, t);
-    } else if (kind == K_LIST) {
-        const uint32_t child = S.list_children[idx];
-        if (child != REF_NONE) {
-            if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-            T.cur = child;
-        }
     } else if constexpr (TIER == TIER_MESH) {
         if (kind == K_TRI || kind == K_QUAD) got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, T.cl.c, t);
     } else if constexpr (FULL) {
@@ -668,6 +693,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         T.cl.set(t);
         record(this_ref, t);
     }
+    if (after != REF_NONE) T.cur = after;
     return true;
 }
 
