@@ -33,9 +33,6 @@ namespace rtk {
 #define RT_BVH4 1
 #endif
 #define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
-#ifndef RT_RARE_KINDS_UNIFORM
-#define RT_RARE_KINDS_UNIFORM 1
-#endif
 // Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
@@ -730,22 +727,18 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, T
 // lane's LDS queue, pq[k * RT_BLOCK], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
 // walked next and the others pushed farthest first.
-template <class Stack>
-__device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
-                                           float tmin_f, float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq,
-                                           uint32_t& pn, Diag& dg) {
+struct Node4Rows {
+    float4 lx, ly, lz, hx, hy, hz, rq;
+};
+__device__ __forceinline__ Node4Rows load_node4(const SceneView& S, uint32_t idx) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
-#ifdef RT_DIAG_LOADLAT
-    const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
-#endif
-    const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], rq = np[6];
-#ifdef RT_DIAG_LOADLAT
-    __builtin_amdgcn_s_waitcnt(0);
-    if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) {
-        dg.load_cyc += __builtin_amdgcn_s_memtime() - tl0;
-        ++dg.loads;
-    }
-#endif
+    return Node4Rows{np[0], np[1], np[2], np[3], np[4], np[5], np[6]};
+}
+// visit4 on node rows already loaded
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
+                                                float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq, uint32_t& pn) {
+    const float4 lx = nr.lx, ly = nr.ly, lz = nr.lz, hx = nr.hx, hy = nr.hy, hz = nr.hz, rq = nr.rq;
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
@@ -790,6 +783,24 @@ __device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, con
     if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
     if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
     return key[0] < INF ? ref[0] : REF_NONE;
+}
+
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
+                                           float tmin_f, float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq,
+                                           uint32_t& pn, Diag& dg) {
+#ifdef RT_DIAG_LOADLAT
+    const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
+#endif
+    const Node4Rows nr = load_node4(S, idx);
+#ifdef RT_DIAG_LOADLAT
+    __builtin_amdgcn_s_waitcnt(0);
+    if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) {
+        dg.load_cyc += __builtin_amdgcn_s_memtime() - tl0;
+        ++dg.loads;
+    }
+#endif
+    return visit4_rows(nr, rf, sf, tmin_f, c_f, stk, sp, pq, pn);
 }
 
 // One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
@@ -850,36 +861,42 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     constexpr uint32_t ROOM = RT_PEND_CAP - 4;  // a visit queues at most 4
     RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
     uint32_t pn = T.pn;
-    if ((T.cur != REF_NONE || T.sp > 0) && pn <= ROOM) {  // node round
+    // The sphere round is decided on the state before this step's node
+    // round and issued first: its sphere load goes out before the node's
+    // seven loads (loads complete in order), and its f64 test runs while the
+    // node is in flight.
+    const bool can = (T.cur != REF_NONE || T.sp > 0) && pn <= ROOM;
+    const unsigned long long mw0 = __ballot(can);
+    const unsigned long long mp0 = __ballot(pn > 0);
+    const bool round = (mw0 == 0 || __popcll(mp0) >= RT_DEFER_THRESH) && pn > 0;
+    // the loads are unconditional (a lane without a round / a node reads
+    // entry 0, cache-hot) so that no branch stands between them and their
+    // waits: the sphere test then waits for its own load only
+    const uint32_t top = pn > 0 ? pn - 1 : 0;
+    const uint32_t sidx = pq[top * RT_BLOCK];
+    pn -= round ? 1u : 0u;
+    const double4 s4 = S.spheres[round ? sidx : 0u];
+    uint32_t cur = REF_NONE;
+    if (can) {
         RT_DIAG_ONLY(++dg.lane_trace_iters;)
         if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
-        const uint32_t cur = T.cur;
+        cur = T.cur;
         T.cur = REF_NONE;
-        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
-#if RT_RARE_KINDS_UNIFORM
-        // lists and standalone spheres are rare (none in C2): one wave-uniform
-        // test skips their code, instead of a divergent switch every round
-        if (__ballot(kind != K_BVH && kind != K_NONE)) {
-            if (kind == K_LIST) {
-                const uint32_t child = S.list_children[idx];
-                if (child != REF_NONE) {
-                    if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                    T.cur = child;
-                }
-            } else if (kind == K_SPHERE) {
-                pq[pn * RT_BLOCK] = idx;
-                ++pn;
-            }
+    }
+    const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+    const Node4Rows rows = load_node4(S, kind == K_BVH ? idx : 0u);
+    if (round) {  // sphere round (sphere.rs:77-108)
+        RT_DIAG_ONLY(++dg.sphere_tests;)
+        double t;
+        if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
+            T.cl.lower(t);
+            T.found = true;
+            T.hit.t = t;
+            T.hit.ref = make_ref(K_SPHERE, sidx);
         }
-        if (kind == K_BVH) {
-            RT_DIAG_ONLY(++dg.node_visits;)
-            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn, dg);
-        }
-#else
-        if (kind == K_BVH) {
-            RT_DIAG_ONLY(++dg.node_visits;)
-            T.cur = visit4(S, idx, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn, dg);
-        } else if (kind == K_LIST) {
+    }
+    if (__ballot(kind != K_BVH && kind != K_NONE)) {  // lists, standalone spheres (none in C2)
+        if (kind == K_LIST) {
             const uint32_t child = S.list_children[idx];
             if (child != REF_NONE) {
                 if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
@@ -889,28 +906,13 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
             pq[pn * RT_BLOCK] = idx;
             ++pn;
         }
-#endif
     }
-    const bool walk = T.cur != REF_NONE || T.sp > 0;
-    const unsigned long long mw = __ballot(walk && pn <= ROOM);
-    const unsigned long long mp = __ballot(pn > 0);
-    if (mw == 0 || __popcll(mp) >= RT_DEFER_THRESH) {
-        if (pn > 0) {  // sphere round (sphere.rs:77-108)
-            RT_DIAG_ONLY(++dg.sphere_tests;)
-            --pn;
-            const uint32_t idx = pq[pn * RT_BLOCK];
-            const double4 s4 = S.spheres[idx];
-            double t;
-            if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
-                T.cl.lower(t);
-                T.found = true;
-                T.hit.t = t;
-                T.hit.ref = make_ref(K_SPHERE, idx);
-            }
-        }
+    if (kind == K_BVH) {
+        RT_DIAG_ONLY(++dg.node_visits;)
+        T.cur = visit4_rows(rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
     }
     T.pn = pn;
-    return walk || pn > 0;
+    return T.cur != REF_NONE || T.sp > 0 || pn > 0;
 }
 
 // ------------------------------------------------------------------ hit record
