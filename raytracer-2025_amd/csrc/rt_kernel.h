@@ -8,7 +8,9 @@
 
 #define RT_BLOCK 256        // 4 waves of 64
 // traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
+#ifndef RT_STACK_BASIC
 #define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
+#endif
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
 #define RT_STACK_MAX 96     // LDS + overflow entries (mesh and full tiers)

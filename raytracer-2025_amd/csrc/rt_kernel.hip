@@ -32,7 +32,9 @@ namespace rtk {
 #ifndef RT_BVH4
 #define RT_BVH4 1
 #endif
+#ifndef RT_PEND_CAP
 #define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
+#endif
 // Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
