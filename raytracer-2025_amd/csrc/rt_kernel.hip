@@ -52,6 +52,7 @@ struct Diag {
     unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0;
     unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
     unsigned long long load_cyc = 0, loads = 0;  // -DRT_DIAG_LOADLAT: node-load latency (first active lane)
+    unsigned long long pops = 0, pop_reads = 0;  // basic tier: pops and the stack entries they read
 #endif
 };
 #ifdef RT_DIAG
@@ -881,7 +882,16 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     uint32_t cur = REF_NONE;
     if (can) {
         RT_DIAG_ONLY(++dg.lane_trace_iters;)
+#ifdef RT_DIAG
+        if (T.cur == REF_NONE) {
+            const uint32_t sp_before = T.sp;
+            T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+            ++dg.pops;
+            dg.pop_reads += sp_before - T.sp;
+        }
+#else
         if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+#endif
         cur = T.cur;
         T.cur = REF_NONE;
     }
@@ -1531,6 +1541,8 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
     atomicAdd(&g_diag[8], (unsigned long long)n_rays);
     atomicAdd(&g_diag[9], dg.load_cyc);
     atomicAdd(&g_diag[10], dg.loads);
+    atomicAdd(&g_diag[11], dg.pops);
+    atomicAdd(&g_diag[12], dg.pop_reads);
 #endif
     atomicAdd(&P->stats[0], (unsigned long long)n_rays);
     if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
@@ -1563,6 +1575,17 @@ RT_TIER_ENTRY(2)
 #endif
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 3
 RT_TIER_ENTRY(3)
+#endif
+#if defined(RT_DIAG) && (!defined(RT_TIER_ONLY) || RT_TIER_ONLY == 0)
+// diagnostic build: the counters live with the (tier 0) kernel that adds to them
+extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_diag), sizeof(unsigned long long) * 16);
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_diag), z, sizeof z);
+    }
+    return (int)e;
+}
 #endif
 #endif
 
@@ -1696,16 +1719,6 @@ extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_
 
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
 
-#ifdef RT_DIAG
-extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_diag), sizeof(unsigned long long) * 16);
-    if (reset) {
-        unsigned long long z[16] = {};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_diag), z, sizeof z);
-    }
-    return (int)e;
-}
-#endif
 
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
     return tier == rtk::TIER_BASIC  ? rtk_occupancy_0(blocks_per_cu)

@@ -55,6 +55,8 @@ out = {
     "node_visits_per_ray": c[6] / c[8],
     "primitive_tests_per_ray": c[7] / c[8],
     "node_load_wave_cycles": c[9] / c[10] if c[10] else None,
-    "raw": c[:11],
+    "stack_reads_per_pop": c[12] / c[11] if c[11] else None,
+    "pops_per_ray": c[11] / c[8],
+    "raw": c[:13],
 }
 print(json.dumps(out, indent=1))
