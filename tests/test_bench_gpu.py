@@ -45,3 +45,23 @@ def test_bench_line_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+
+
+def test_bench_two_ranks_gloo():
+    """The N > 1 path (torch.distributed.run, rows interleaved, frame gathered
+    to rank 0) with 2 ranks sharing the one GPU over gloo: one JSON line from
+    rank 0, n_gpus 2, the whole frame's samples."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--width", "256", "--spp", "16",
+                        "--backend", "gloo", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["frame_samples"] == 256 * 144 * 16 and d["value"] > 0
