@@ -6,10 +6,20 @@
 
 #include "rt_layout.h"
 
-#define RT_BLOCK 256        // 4 waves of 64
-// traversal-stack entries per lane; LDS = entries * RT_BLOCK * 8 B per block
+#define RT_BLOCK 256        // 4 waves of 64 (mesh and full tiers)
+// Basic tier: one 1024-thread block per CU (16 waves, 4 per SIMD: the same
+// 128-VGPR budget) so that one LDS copy of the world's 4-wide nodes serves
+// the whole CU.  LDS: stack entries * 1024 * 8 B + the sphere queue
+// (RT_PEND_CAP * 1024 * 2 B) + RT_NODE_LDS_BYTES of nodes <= 160 KiB.
+#ifndef RT_BLOCK_BASIC
+#define RT_BLOCK_BASIC 1024
+#endif
+// traversal-stack entries per lane; LDS = entries * block * 8 B
 #ifndef RT_STACK_BASIC
-#define RT_STACK_BASIC 16   // 32 KiB: 4 blocks per CU (VGPR-bound at 128)
+#define RT_STACK_BASIC 14   // 112 KiB of the basic tier's 1024-lane block
+#endif
+#ifndef RT_NODE_LDS_BYTES
+#define RT_NODE_LDS_BYTES 32704  // basic tier: the first 292 DNode4 of the world in LDS
 #endif
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
@@ -59,3 +69,5 @@ extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_
 // device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);
+// threads per block of a tier's path kernel
+extern "C" int rtk_block_threads(int tier);

@@ -33,7 +33,7 @@ namespace rtk {
 #define RT_BVH4 1
 #endif
 #ifndef RT_PEND_CAP
-#define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 4 B each)
+#define RT_PEND_CAP 8  // queued sphere tests per lane (LDS, 2 B each: sphere index < 65536)
 #endif
 // Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
 #ifndef RT_MESH_BVH4
@@ -298,7 +298,7 @@ struct HitInfo {
 // per half-wave.  With OVF, entries k >= CAP (deep triangle BVHs) live in the
 // lane's column of a global overflow buffer, [k - CAP][lane of the grid], so
 // the LDS part stays small enough for 4 blocks per CU.
-template <uint32_t CAP, bool OVF>
+template <uint32_t CAP, bool OVF, uint32_t BLK>
 struct StackT {
     uint2* base;
     RT_GLOBAL uint2* ovf;
@@ -308,16 +308,16 @@ struct StackT {
         if (OVF && sp >= CAP)
             ovf[(sp - CAP) * stride] = v;
         else
-            base[sp * RT_BLOCK] = v;
+            base[sp * BLK] = v;
     }
     __device__ __forceinline__ uint2 at(uint32_t sp) const {
         if (OVF && sp >= CAP) return ovf[(sp - CAP) * stride];
-        return base[sp * RT_BLOCK];
+        return base[sp * BLK];
     }
 };
 template <int TIER>
 using StackFor = StackT<tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
-                        TIER != TIER_BASIC>;
+                        TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
 
 // Closest-hit state of one traversal: t and its f32 upper bound.
 struct Closest {
@@ -727,20 +727,26 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, T
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
-// lane's LDS queue, pq[k * RT_BLOCK], when the exact test must run), then the
+// lane's LDS queue, pq[k * RT_BLOCK_BASIC], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
 // walked next and the others pushed farthest first.
 struct Node4Rows {
     float4 lx, ly, lz, hx, hy, hz, rq;
 };
-__device__ __forceinline__ Node4Rows load_node4(const SceneView& S, uint32_t idx) {
-    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
+constexpr uint32_t NODE_LDS_CAP = RT_NODE_LDS_BYTES / sizeof(DNode4);
+// The node rows from the block's LDS copy: the launcher gives the basic tier
+// only worlds whose whole 4-wide tree fits it (NODE_LDS_CAP nodes: about 900
+// spheres; larger sphere worlds run the mesh tier).  A per-wave
+// fallback to global reads for larger trees cost 88 B/lane of scratch at the
+// 128-VGPR budget.
+__device__ __forceinline__ Node4Rows load_node4(const float4* nl, uint32_t idx) {
+    const float4* np = nl + idx * 7u;
     return Node4Rows{np[0], np[1], np[2], np[3], np[4], np[5], np[6]};
 }
 // visit4 on node rows already loaded
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
-                                                float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq, uint32_t& pn) {
+                                                float& c_f, Stack& stk, uint32_t& sp, uint16_t* pq, uint32_t& pn) {
     const float4 lx = nr.lx, ly = nr.ly, lz = nr.lz, hx = nr.hx, hy = nr.hy, hz = nr.hz, rq = nr.rq;
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -752,7 +758,7 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
-                pq[pn * RT_BLOCK] = ref_index(R[i]);
+                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_index(R[i]);
                 ++pn;
             }
         }
@@ -786,24 +792,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
     if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
     if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
     return key[0] < INF ? ref[0] : REF_NONE;
-}
-
-template <class Stack>
-__device__ __forceinline__ uint32_t visit4(const SceneView& S, uint32_t idx, const RayF& rf, const SphF& sf,
-                                           float tmin_f, float& c_f, Stack& stk, uint32_t& sp, uint32_t* pq,
-                                           uint32_t& pn, Diag& dg) {
-#ifdef RT_DIAG_LOADLAT
-    const unsigned long long tl0 = __builtin_amdgcn_s_memtime();
-#endif
-    const Node4Rows nr = load_node4(S, idx);
-#ifdef RT_DIAG_LOADLAT
-    __builtin_amdgcn_s_waitcnt(0);
-    if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) {
-        dg.load_cyc += __builtin_amdgcn_s_memtime() - tl0;
-        ++dg.loads;
-    }
-#endif
-    return visit4_rows(nr, rf, sf, tmin_f, c_f, stk, sp, pq, pn);
 }
 
 // One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
@@ -858,7 +846,7 @@ __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t id
 // trace_step's walk (A/B renders: RMSE 0).
 template <class Stack>
 __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
-                                            uint32_t* pq, Diag& dg) {
+                                            uint16_t* pq, const float4* nl, Diag& dg) {
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
     constexpr uint32_t ROOM = RT_PEND_CAP - 4;  // a visit queues at most 4
@@ -876,7 +864,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     // entry 0, cache-hot) so that no branch stands between them and their
     // waits: the sphere test then waits for its own load only
     const uint32_t top = pn > 0 ? pn - 1 : 0;
-    const uint32_t sidx = pq[top * RT_BLOCK];
+    const uint32_t sidx = pq[top * RT_BLOCK_BASIC];
     pn -= round ? 1u : 0u;
     const double4 s4 = S.spheres[round ? sidx : 0u];
     uint32_t cur = REF_NONE;
@@ -896,7 +884,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
         T.cur = REF_NONE;
     }
     const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
-    const Node4Rows rows = load_node4(S, kind == K_BVH ? idx : 0u);
+    const Node4Rows rows = load_node4(nl, kind == K_BVH ? idx : 0u);
     if (round) {  // sphere round (sphere.rs:77-108)
         RT_DIAG_ONLY(++dg.sphere_tests;)
         double t;
@@ -915,7 +903,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
                 T.cur = child;
             }
         } else if (kind == K_SPHERE) {
-            pq[pn * RT_BLOCK] = idx;
+            pq[pn * RT_BLOCK_BASIC] = (uint16_t)idx;
             ++pn;
         }
     }
@@ -1354,20 +1342,30 @@ struct KParams {
 };
 
 template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+__global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
     const Frame& F = P->F;
     uint32_t* queue = P->queue;
     constexpr int STACK = tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
-    __shared__ uint2 stack_lds[STACK * RT_BLOCK];
+    constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
+    __shared__ uint2 stack_lds[STACK * BLK];
     __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
     uint4* med = media_lds + threadIdx.x;
-    __shared__ uint32_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * RT_BLOCK : 1];
-    uint32_t* pq = pend_lds + threadIdx.x;
+    __shared__ uint16_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * BLK : 1];
+    uint16_t* pq = pend_lds + threadIdx.x;
     StackFor<TIER> stk{stack_lds + threadIdx.x,
-                       P->stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x, gridDim.x * RT_BLOCK};
+                       P->stack_ovf + (uint64_t)blockIdx.x * BLK + threadIdx.x, gridDim.x * BLK};
+    // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
+    // 241 nodes for C1/C2), read by every node visit instead of global memory.
+    __shared__ float4 node_lds[TIER == TIER_BASIC && RT_BVH4 ? NODE_LDS_CAP * 7 : 1];
+    if constexpr (TIER == TIER_BASIC && RT_BVH4) {
+        const uint32_t n_lds = min(S.n_nodes4, NODE_LDS_CAP);  // == n_nodes4 (launcher)
+        const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
+        for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) node_lds[k] = src[k];
+        __syncthreads();
+    }
     const uint32_t lane = __lane_id();
 
     Rng rng;
@@ -1403,7 +1401,7 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
 #if RT_QUEUE_GUIDE
             {
                 const uint32_t left = F.total_items > pool_end ? F.total_items - pool_end : 0u;
-                const uint32_t g = left / (gridDim.x * (RT_BLOCK / 64) * RT_QUEUE_GUIDE);
+                const uint32_t g = left / (gridDim.x * (BLK / 64) * RT_QUEUE_GUIDE);
                 chunk = g < 64u ? 64u : (g > (uint32_t)RT_QUEUE_CHUNK ? (uint32_t)RT_QUEUE_CHUNK : g);
             }
 #endif
@@ -1476,7 +1474,7 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
                             : (TIER == TIER_MESH ? RT_SHADE_BATCH_MESH : RT_SHADE_BATCH_FULL);
         auto step = [&]() -> bool {
             if constexpr (TIER == TIER_BASIC && RT_BVH4) {
-                return trace4_step(S, ray, T, stk, pq, dg);
+                return trace4_step(S, ray, T, stk, pq, node_lds, dg);
             } else {
                 RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
                 return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
@@ -1557,11 +1555,12 @@ __global__ void __launch_bounds__(RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAV
 // it whole.
 #define RT_TIER_ENTRY(N)                                                                                        \
     extern "C" hipError_t rtk_launch_path_##N(int grid, hipStream_t stream, const rtk::KParams* P) {          \
-        hipLaunchKernelGGL(rtk::rt_path_kernel<N>, dim3(grid), dim3(RT_BLOCK), 0, stream, P);               \
+        hipLaunchKernelGGL(rtk::rt_path_kernel<N>, dim3(grid), dim3(N == 0 ? RT_BLOCK_BASIC : RT_BLOCK), 0, stream, P); \
         return hipGetLastError();                                                                            \
     }                                                                                                        \
     extern "C" int rtk_occupancy_##N(int* blocks_per_cu) {                                                   \
-        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<N>, RT_BLOCK, 0); \
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_path_kernel<N>,            \
+                                                                 N == 0 ? RT_BLOCK_BASIC : RT_BLOCK, 0);         \
     }
 #if !defined(RT_COMMON_ONLY)
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 0
@@ -1657,6 +1656,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 }
 
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
+extern "C" int rtk_block_threads(int tier) { return tier == rtk::TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }
 extern "C" int rtk_full_bvh4(void) { return RT_FULL_BVH4; }
 

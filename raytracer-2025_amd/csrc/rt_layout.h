@@ -203,6 +203,7 @@ struct SceneView {
     int32_t background_tex;  // -1 = black
     uint32_t stack_need;     // max traversal stack entries (host-computed)
     uint32_t features;       // F_* of everything reachable from world/lights
+    uint32_t n_nodes4;       // entries of nodes4
 };
 
 // Scene features; the launcher picks the smallest kernel tier covering them.

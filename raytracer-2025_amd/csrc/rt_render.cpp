@@ -66,7 +66,11 @@ void destroy_device_world(DeviceWorld* d) {
 // -1 with RT_ESTACK set).
 static int prepare_tier(HostWorld& hw) {
     int tier = rtk_tier_for(hw.features, hw.stack_need);
-    if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() && bvh4_convert(hw, RT_STACK_BASIC, true) > RT_STACK_BASIC)
+    // the basic tier queues sphere indices as 16-bit LDS entries
+    if (tier == rtk::TIER_BASIC && hw.spheres.size() > 65536) tier = rtk::TIER_MESH;
+    // the basic tier's kernel reads every 4-wide node from its LDS copy
+    if (tier == rtk::TIER_BASIC && rtk_basic_bvh4() &&
+        bvh4_convert(hw, RT_STACK_BASIC, true, RT_NODE_LDS_BYTES / sizeof(rtk::DNode4)) > RT_STACK_BASIC)
         tier = rtk::TIER_MESH;
     if (tier == rtk::TIER_MESH && rtk_mesh_bvh4() && bvh4_convert(hw, RT_STACK_MAX, false) > RT_STACK_MAX)
         tier = rtk::TIER_FULL;
@@ -195,6 +199,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     v.background_tex = bg;
     v.stack_need = hw.stack_need;
     v.features = hw.features;
+    v.n_nodes4 = (uint32_t)hw.nodes4.size();
     d->tier = tier;
     d->reference_bvh = reference_bvh;
     d->blob_bytes = blob.size();

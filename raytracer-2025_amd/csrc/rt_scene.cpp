@@ -1090,7 +1090,7 @@ namespace rth {
 // children - 1) + max need(inner child); otherwise (mesh tier) a sphere child
 // gets its box rounded outward and, like every child, is walked near-first
 // through the stack: need(node) = (children - 1) + max need(child).
-uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres) {
+uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes) {
     using rtk::REF_NONE;
     struct Child {
         uint32_t ref;
@@ -1214,6 +1214,7 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres) {
     };
     const uint32_t sn = 1 + need(root);
     if (sn > max_need) return sn;
+    if (out.size() > max_nodes) return UINT32_MAX;
     hw.nodes4 = std::move(out);
     hw.nodes.clear();  // the two-box nodes are not walked any more
     hw.list_children = std::move(lists);

@@ -158,7 +158,8 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 // Collapses every two-box BVH into 4-wide nodes (hw.nodes4; sphere children as
 // filter records when filter_spheres, the basic tier), rewrites the K_BVH refs
 // to index nodes4 and recomputes stack_need.  Returns the new stack_need (hw is
-// unchanged when it exceeds max_need).
-uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres);
+// unchanged when it exceeds max_need), or UINT32_MAX (hw unchanged) when the
+// tree would have more than max_nodes nodes.
+uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes = SIZE_MAX);
 void destroy_device_world(DeviceWorld* d);
 }  // namespace rth

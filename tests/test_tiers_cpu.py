@@ -14,7 +14,7 @@ import tempfile
 
 import pytest
 
-STACK_BASIC = 16  # RT_STACK_BASIC (raytracer-2025_amd/csrc/rt_kernel.h)
+STACK_BASIC = 14  # RT_STACK_BASIC (raytracer-2025_amd/csrc/rt_kernel.h)
 STACK_MAX = 96    # RT_STACK_MAX
 
 
