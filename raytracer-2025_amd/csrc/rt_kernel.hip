@@ -1575,8 +1575,8 @@ RT_TIER_ENTRY(2)
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 3
 RT_TIER_ENTRY(3)
 #endif
-#if defined(RT_DIAG) && (!defined(RT_TIER_ONLY) || RT_TIER_ONLY == 0)
-// diagnostic build: the counters live with the (tier 0) kernel that adds to them
+#if defined(RT_DIAG)
+// diagnostic build: the counters live with the (DIAG_TIER) kernel that adds to them
 extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
     hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_diag), sizeof(unsigned long long) * 16);
     if (reset) {

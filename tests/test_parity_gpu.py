@@ -414,3 +414,33 @@ def test_sphere_bvh_edge_worlds(gpu, oracle, rt, capi, n, variant):
     info = capi.RtWorldInfo()
     assert gpu.world_info_get(s.s, w.h, -1, cam.background.h, 0, ctypes.byref(info)) == 0
     assert info.kernel_tier == (1 if variant == "mesh" else 0)
+
+
+def _many_spheres_world(s, n):
+    import random
+    rnd = random.Random(n)
+    mats = [s.Lambertian(s.SolidColor((0.7, 0.3, 0.2))), s.Metal((0.8, 0.8, 0.9), 0.1),
+            s.Dielectric(s.SolidColor((1.0, 1.0, 1.0)), 1.5), s.Lambertian(s.SolidColor((0.2, 0.6, 0.3)))]
+    objs = s.Hittables()
+    objs.add(s.Sphere((0.0, -1000.0, 0.0), 1000.0, mats[0]))
+    for i in range(n):
+        objs.add(s.Sphere((rnd.uniform(-4, 4), 0.1, rnd.uniform(-6, 3)), 0.1, mats[i % 4]))
+    w = s.Hittables()
+    w.add(s.BVH(objs))
+    return w, None, rt_camera(s, 48, 16)
+
+
+@pytest.mark.parametrize("n", [300, 3000])
+def test_sphere_worlds_around_the_lds_tree_limit(gpu, oracle, rt, capi, n):
+    """A sphere BVH whose 4-wide tree fits the basic tier's LDS copy (300
+    spheres) and one that does not and runs the mesh tier (3000), against the
+    oracle."""
+    import ctypes
+    out, st = render_both(gpu, oracle, rt, lambda s: _many_spheres_world(s, n))
+    check(out, min_exact=0.97)
+    assert st["gpu"].panics == 0
+    s = rt.Scene(gpu)
+    w, _, cam = _many_spheres_world(s, n)
+    info = capi.RtWorldInfo()
+    assert gpu.world_info_get(s.s, w.h, -1, cam.background.h, 0, ctypes.byref(info)) == 0
+    assert info.kernel_tier == (0 if n == 300 else 1)

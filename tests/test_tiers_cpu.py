@@ -96,3 +96,29 @@ def test_small_sphere_bvhs(product, capi, rt, n):
     assert info.kernel_tier == 0
     assert info.primitives == n
     assert max(1, -(-(n - 1) // 3)) <= info.bvh_nodes <= max(1, n - 1)
+
+
+NODE_LDS_CAP = 32704 // 112  # RT_NODE_LDS_BYTES / sizeof(DNode4): the basic tier's LDS copy of the tree
+
+
+@pytest.mark.parametrize("n", [600, 3000])
+def test_basic_tier_tree_fits_lds(product, capi, rt, n):
+    """The basic tier reads every 4-wide node from the block's LDS copy, so it
+    takes a sphere BVH only while its tree has at most NODE_LDS_CAP nodes; a
+    larger one runs the mesh tier (all children boxed)."""
+    import random
+    rnd = random.Random(n)
+    s = rt.Scene(product)
+    mat = s.Lambertian(s.SolidColor((0.5, 0.5, 0.5)))
+    objs = s.Hittables()
+    for _ in range(n):
+        objs.add(s.Sphere((rnd.uniform(-50, 50), rnd.uniform(0, 5), rnd.uniform(-50, 50)), 0.2, mat))
+    w = s.Hittables()
+    w.add(s.BVH(objs))
+    info = info_of(product, capi, s, w)
+    if info.kernel_tier == 0:
+        assert info.bvh_nodes <= NODE_LDS_CAP
+    else:
+        assert info.kernel_tier == 1
+        assert info.bvh_nodes > NODE_LDS_CAP or info.stack_need > STACK_BASIC
+    assert info.kernel_tier == (0 if n == 600 else 1)
