@@ -1302,7 +1302,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_BASIC_WAVES 4  // waves per SIMD the basic tier is register-allocated for
 #endif
 #ifndef RT_FULL_WAVES
-#define RT_FULL_WAVES 3  // 3 waves with some spills beat 2 without: C3 -13 %, C5 -19 %
+#define RT_FULL_WAVES 2  // full tier (C5): 2 waves without spills, shading in batches of 56 (below)
 #endif
 #ifndef RT_FLAT_WAVES
 #define RT_FLAT_WAVES 3  // FULL_FLAT
@@ -1318,7 +1318,14 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_SHADE_BATCH_MESH 48
 #endif
 #ifndef RT_SHADE_BATCH_FULL
-#define RT_SHADE_BATCH_FULL 64
+// C5 walks are uneven (37 % lane efficiency with whole-wave shading): at 2
+// waves/SIMD the 256-VGPR budget holds the walk state across a shading batch
+// without spills, C5 -12 % against 3 waves / whole-wave shading; at 3 waves
+// batches spill 372 B/lane and cost +65 %
+#define RT_SHADE_BATCH_FULL 56
+#endif
+#ifndef RT_SHADE_BATCH_FLAT
+#define RT_SHADE_BATCH_FLAT 64
 #endif
 #ifndef RT_QUEUE_CHUNK
 #define RT_QUEUE_CHUNK 256  // most items a wave takes per queue atomic (>= 64)
@@ -1471,7 +1478,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         }
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
-                            : (TIER == TIER_MESH ? RT_SHADE_BATCH_MESH : RT_SHADE_BATCH_FULL);
+                            : TIER == TIER_MESH ? RT_SHADE_BATCH_MESH
+                            : TIER == TIER_FULL ? RT_SHADE_BATCH_FULL : RT_SHADE_BATCH_FLAT;
         auto step = [&]() -> bool {
             if constexpr (TIER == TIER_BASIC && RT_BVH4) {
                 return trace4_step(S, ray, T, stk, pq, node_lds, dg);
