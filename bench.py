@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Headline benchmark: Msamples/s on the book-1 random-spheres scene at
-1920x1080, "512 spp" (= 22^2 = 484 traced strata, camera.rs:212), max_depth 50,
+1920x1080, "512 spp" (= 22^2 = 484 traced strata, camera.rs:212), max_depth 50 (C3: 10, C5: 40),
 f64 -- BASELINE.json configs[1] (C2) on 1..8 MI355X.
 
 A step renders one whole frame: every rank renders its interleaved rows
@@ -257,7 +257,7 @@ def main():
                      "c5": "the reference's final_scene (main.rs:384-539), randomness from SplitMix64(2025)"}[args.workload]
                     + ", render RNG seed " + str(args.seed),
             "config": {
-                "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth 50, "
+                "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth {cam.max_depth}, "
                             "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
                 "frame_samples": frame_samples,
                 "parallelism": f"row-shard x{world_size}",
