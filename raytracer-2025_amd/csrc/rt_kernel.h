@@ -23,6 +23,12 @@
 #endif
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
+#ifndef RT_STACK_FLAT
+#define RT_STACK_FLAT 8     // full-flat tier (lists only: C3 needs few entries); deeper ones overflow
+#endif
+#ifndef RT_FLAT_LDS_STATE
+#define RT_FLAT_LDS_STATE 1 // full-flat tier: beta, L, acc and the item fields live in LDS across the walk
+#endif
 #define RT_STACK_MAX 96     // LDS + overflow entries (mesh and full tiers)
 #ifndef RT_MEDIA_CAP
 #define RT_MEDIA_CAP 2      // full tier: media a walk queues (in LDS, 16 B each) before testing them inline
@@ -40,6 +46,10 @@ namespace rtk {
 enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2, TIER_FULL_FLAT = 3 };
 constexpr int N_TIERS = 4;
 __host__ __device__ constexpr bool tier_full(int t) { return t >= TIER_FULL; }
+// traversal-stack entries a lane keeps in LDS (deeper ones: global overflow column)
+__host__ __device__ constexpr uint32_t lds_stack_entries(int t) {
+    return t == TIER_BASIC ? RT_STACK_BASIC : t == TIER_MESH ? RT_STACK_MESH : t == TIER_FULL ? RT_STACK_FULL : RT_STACK_FLAT;
+}
 }  // namespace rtk
 
 // Camera::initilize results (camera.rs:204-245) for one shard.

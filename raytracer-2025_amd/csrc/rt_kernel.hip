@@ -316,8 +316,7 @@ struct StackT {
     }
 };
 template <int TIER>
-using StackFor = StackT<tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC),
-                        TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
+using StackFor = StackT<lds_stack_entries(TIER), TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
 
 // Closest-hit state of one traversal: t and its f32 upper bound.
 struct Closest {
@@ -1355,7 +1354,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     const SceneView S = P->S;
     const Frame& F = P->F;
     uint32_t* queue = P->queue;
-    constexpr int STACK = tier_full(TIER) ? RT_STACK_FULL : (TIER == TIER_MESH ? RT_STACK_MESH : RT_STACK_BASIC);
+    constexpr int STACK = lds_stack_entries(TIER);
     constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
     __shared__ uint2 stack_lds[STACK * BLK];
     __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
@@ -1374,6 +1373,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         __syncthreads();
     }
     const uint32_t lane = __lane_id();
+    // Full-flat tier: the path state the walk never reads (beta, L, acc, the
+    // item's fields) is parked in LDS across the walk, so that its registers
+    // are free there instead of spilled to scratch around it.
+    constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
+    __shared__ double pstate_lds[LDS_STATE ? 9 * RT_BLOCK : 1];
+    __shared__ uint4 pitem_lds[LDS_STATE ? RT_BLOCK : 1];
+    double* pst = pstate_lds + threadIdx.x;
+    uint4* pit = pitem_lds + threadIdx.x;
 
     Rng rng;
     rng.k0 = F.key0;
@@ -1489,8 +1496,21 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             }
         };
         if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
+            if constexpr (LDS_STATE) {
+                pst[0 * RT_BLOCK] = beta.x, pst[1 * RT_BLOCK] = beta.y, pst[2 * RT_BLOCK] = beta.z;
+                pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
+                pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
+                *pit = make_uint4(item, s_j, px, py);
+            }
             while (walking) walking = step();
             if constexpr (tier_full(TIER)) media_phase<TIER>(S, ray, T, stk, rng, med);
+            if constexpr (LDS_STATE) {
+                beta = d3(pst[0 * RT_BLOCK], pst[1 * RT_BLOCK], pst[2 * RT_BLOCK]);
+                L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
+                acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
+                const uint4 it = *pit;
+                item = it.x, s_j = it.y, px = it.z, py = it.w;
+            }
         } else {
             const unsigned long long active = __ballot(true);
             for (;;) {

@@ -145,7 +145,7 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     if (hw.stack_need > stack_cap)
         return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
                                         std::to_string(stack_cap));
-    const uint32_t lds_entries = tier == rtk::TIER_BASIC ? RT_STACK_BASIC : (tier == rtk::TIER_MESH ? RT_STACK_MESH : RT_STACK_FULL);
+    const uint32_t lds_entries = rtk::lds_stack_entries(tier);
     if (hw.stack_need > lds_entries) {
         const size_t need = (size_t)(hw.stack_need - lds_entries) * d->grid[tier] * RT_BLOCK * sizeof(uint64_t);
         if (need > d->stack_ovf_bytes) {
