@@ -24,6 +24,7 @@ run bench_c3 400 python3 bench.py --workload c3 --steps 3 --warmup 1
 if [ -n "${BENCH_C5:-}" ]; then run bench_c5 900 python3 bench.py --workload c5 --steps 1 --warmup 1; fi
 for w in ${PROFILE_WORKLOADS:-c2 c4 c3}; do
   B="bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline"
+  if [ "$w" = c5 ]; then B="bench.py --workload c5 --steps 1 --warmup 0 --no-cpu-baseline"; fi  # ~51 s frames
   run trace_$w 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$w -o run -- python3 $B
   run fetch_$w 400 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $OUT/fetch_$w -o run -- python3 $B
   run write_$w 400 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $OUT/write_$w -o run -- python3 $B
