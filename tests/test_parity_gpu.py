@@ -56,6 +56,28 @@ def test_c1_full_config(gpu, oracle, rt, scenes):
     assert st["gpu"].samples == 400 * 225 * 100
 
 
+def test_c2_full_config_rows(gpu, oracle, rt, scenes):
+    """BASELINE configs[1] (the bench workload): book-1 random spheres at
+    1920x1080, 512 spp (22^2 = 484 traced), depth 50.  Five shard rows (every
+    216th) against the oracle at the full sample count, and the whole frame on
+    the GPU for its sample count, finiteness and no panics."""
+    out = {}
+    for name, api in (("gpu", gpu), ("oracle", oracle)):
+        scene = rt.Scene(api)
+        world, lights, cam = scenes.random_spheres(scene, 1920, 512)
+        assert (cam.image_height, cam.sqrt_spp, cam.max_depth) == (1080, 22, 50)
+        lin, _, st = cam.render(world, lights, seed=1, row_offset=0, row_stride=216)
+        assert lin.shape == (5, 1920, 3) and st.samples == 5 * 1920 * 484 and st.panics == 0
+        out[name] = (lin, None)
+        if name == "gpu":
+            full, _, st1 = cam.render(world, lights, seed=1, want_srgb=False)
+            assert full.shape == (1080, 1920, 3) and np.isfinite(full).all()
+            assert st1.samples == 1920 * 1080 * 484 and st1.panics == 0
+            # rows 0, 216, ... of the whole frame are the shard's rows
+            assert np.array_equal(full[::216], lin)
+    check(out, min_exact=0.99)
+
+
 def test_c3_cornell_smoke_small(gpu, oracle, rt, scenes):
     """Quads, Transform, ConstantMedium, Isotropic, DiffuseLight, light-PDF mixture (C3 features)."""
     out, _ = render_both(gpu, oracle, rt, lambda s: scenes.cornell_smoke(s, 96, 16))
