@@ -31,6 +31,9 @@ namespace rtk {
 #ifndef RT_SLAB_FOLD
 #define RT_SLAB_FOLD 1
 #endif
+#ifndef RT_RCP_F32
+#define RT_RCP_F32 1
+#endif
 
 #if RT_SLAB_FOLD
 // The t-interval widening folded into the ray: the plane distances of the
@@ -50,9 +53,16 @@ RT_HD RayF make_rayf(const double o[3], const double d[3]) {
     RayF R;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double id = 1.0 / d[k];
-        float f = (float)id;
-        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, (float)id);
+#if RT_RCP_F32
+        // d rounded to f32, then the correctly rounded f32 quotient: < 1.01u
+        // relative (the f64 quotient rounded once: 0.5u).  The error is
+        // common to both plane distances of the axis, a relative error of t,
+        // inside the 2^-21 widening with the other roundings.
+        float f = 1.0f / (float)d[k];
+#else
+        float f = (float)(1.0 / d[k]);
+#endif
+        if (!(fabsf(f) <= 1.152921504606847e18f)) f = copysignf(1.152921504606847e18f, f);
         const float of = (float)o[k];
         const float pad = fabsf(of) * 4.76837158203125e-07f + 1e-30f;  // 2^-21 |o|
         constexpr float SHRINK = 1.0f - 4.76837158203125e-07f, GROW = 1.0f + 4.76837158203125e-07f;

@@ -16,16 +16,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
 
 
-@pytest.mark.parametrize("fold", [1, 0])
+@pytest.mark.parametrize("fold,rcp", [(1, 0), (1, 1), (0, 0)])
 @pytest.mark.parametrize("contract", ["fast", "off"])
 @pytest.mark.parametrize("seed", [2025, 7])
-def test_slab_is_conservative(contract, seed, fold):
+def test_slab_is_conservative(contract, seed, fold, rcp):
     """fold = 1: the kernel's default (widening folded into the ray, RT_SLAB_FOLD);
-    0: the widening applied per test."""
+    0: the widening applied per test.  rcp = 1: 1/d as an f32 quotient of d
+    rounded to f32 (RT_RCP_F32) instead of the f64 quotient rounded once."""
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "slab_prop_%s_%d" % (contract, fold))
+    exe = os.path.join(BUILD, "slab_prop_%s_%d_%d" % (contract, fold, rcp))
     flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
-    flags.append("-DRT_SLAB_FOLD=%d" % fold)
+    flags += ["-DRT_SLAB_FOLD=%d" % fold, "-DRT_RCP_F32=%d" % rcp]
     subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "slab_prop.cpp"), "-o", exe],
                    check=True)
     r = subprocess.run([exe, "1500000", str(seed)], capture_output=True, text=True, timeout=300)
