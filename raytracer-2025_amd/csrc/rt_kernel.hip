@@ -1333,7 +1333,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_QUEUE_GUIDE 8  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
 #endif
 #ifndef RT_MESH_WAVES
-#define RT_MESH_WAVES 4  // 4-wave budget (some spills) beats 2 waves: 164.7 vs 263.8 ms (C4, 64 spp)
+#define RT_MESH_WAVES 4  // beats 2 waves (164.7 vs 263.8 ms, C4 64 spp) and 3 / 5 waves (+16 % / +12 %)
 #endif
 
 // Launch parameters live in device memory and are read where they are used
