@@ -3,16 +3,20 @@
 1920x1080, "512 spp" (= 22^2 = 484 traced strata, camera.rs:212), max_depth 50 (C3: 10, C5: 40),
 f64 -- BASELINE.json configs[1] (C2) on 1..8 MI355X.
 
-A step renders one whole frame: every rank renders its interleaved rows
-(row_offset = rank, row_stride = N) with the gfx950 kernel through the C ABI
-(rt_render_device on torch's current stream), then the linear framebuffer is
-gathered to rank 0 over RCCL (N > 1).  Scaling is strong: the frame is fixed,
+A step renders one whole frame through the C ABI (rt_render_device on
+torch's current stream).  With N > 1 ranks (torch.distributed.run, one
+process per GPU) every rank passes the library an RCCL communicator
+(rt_comm_init; the unique id travels over the torch process group): rank r
+renders the rows r, r + N, ... and the library gathers the linear framebuffer
+to rank 0 in one ncclSend/ncclRecv group.  --in-process drives N devices from
+one process (rt_render_opts.devices).  Scaling is strong: the frame is fixed,
 ranks split it.  value = traced samples of all steps / max-over-ranks time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
   python bench.py --workload c4        # BASELINE configs[3]: 1M-triangle OBJ, 1920x1080, 256 spp
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --in-process
 """
 import argparse
 import ctypes
@@ -29,6 +33,30 @@ PKG = "raytracer-2025_amd"
 
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec (half the 157.3 TF f32 vector rate)
 HBM_PEAK_GBS = 8000.0
+
+
+def usable_cpus():
+    """The host CPUs this job may run on: the affinity mask, capped by a cgroup
+    CPU quota when one is set (a GPU box gives a job a share of a large host;
+    os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(-(-int(q) // int(per))))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, -(-q // per))
+        except (OSError, ValueError):
+            pass
+    return (min(n, quota) if quota else n), {"affinity": n, "cgroup_quota": quota, "os_cpu_count": os.cpu_count()}
 
 
 def cpu_model():
@@ -68,20 +96,7 @@ def build_workload(scenes, scene, workload, width, spp):
     return world, lights, cam, "C4: synthetic 1M-triangle OBJ terrain (999 698 triangles, 2 models) + 2 spheres"
 
 
-def cpu_baseline(threads, row_stride, spp, workload="c2"):
-    """The TEST-ONLY oracle (reference algorithm, f64, recursive ray_color,
-    reference BVH topology) on the host cores: a bounded sample of the same
-    C2 workload -- every `row_stride`-th row of the 1920x1080 frame at `spp`
-    (sqrt_spp^2 strata).  Per-sample cost does not depend on spp."""
-    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
-    if not os.path.exists(so):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
-    capi = importlib.import_module(PKG + ".capi")
-    rt = importlib.import_module(PKG + ".raytracer")
-    scenes = importlib.import_module(PKG + ".scenes")
-    api = capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
-    scene = rt.Scene(api)
-    world, lights, cam, desc = build_workload(scenes, scene, workload, WORKLOADS[workload][0], spp)
+def _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads):
     c = cam.to_c()
     opts = capi.RtRenderOpts()
     api.render_opts_default(ctypes.byref(opts))
@@ -93,27 +108,71 @@ def cpu_baseline(threads, row_stride, spp, workload="c2"):
     t0 = time.perf_counter()
     api.check(api.render_f64(scene.s, world.h, -1 if lights is None else lights.h, ctypes.byref(c), ctypes.byref(opts),
                              None, None, ctypes.byref(st), None))
-    dt = time.perf_counter() - t0
-    return {
-        "value": st.samples / dt / 1e6,
+    return st.samples, time.perf_counter() - t0
+
+
+def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
+    """The TEST-ONLY oracle (reference algorithm, f64, recursive ray_color,
+    reference BVH topology, pixels over `threads` host threads as rayon does)
+    on the host: a bounded sample of the same workload -- every
+    `row_stride`-th row of the frame at `spp` (sqrt_spp^2 strata); per-sample
+    cost does not depend on spp.  For C2 also BASELINE configs[0] in full
+    (book-1 random spheres 400x225, 100 spp), as BASELINE.md plans."""
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
+    capi = importlib.import_module(PKG + ".capi")
+    rt = importlib.import_module(PKG + ".raytracer")
+    scenes = importlib.import_module(PKG + ".scenes")
+    api = capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
+    scene = rt.Scene(api)
+    world, lights, cam, desc = build_workload(scenes, scene, workload, WORKLOADS[workload][0], spp)
+    samples, dt = _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads)
+    info = cpu_info or {}
+    res = {
+        "value": samples / dt / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{desc.split(':')[0]} scene, every {row_stride}th row of {cam.image_width}x{cam.image_height} at {spp} spp ({cam.sqrt_spp**2} traced), "
-                  f"{st.samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
-                  "(oracle/: reference-semantics C++ restatement, not the Rust binary)",
+                  f"{samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
+                  f"(all CPUs this job may use: affinity {info.get('affinity')}, cgroup quota {info.get('cgroup_quota')}, "
+                  f"os.cpu_count {info.get('os_cpu_count')}; oracle/: reference-semantics C++ restatement, not the Rust binary)",
     }
+    if workload == "c2":
+        s1 = rt.Scene(api)
+        w1, l1, cam1 = scenes.random_spheres(s1, 400, 100)
+        n1, dt1 = _oracle_render(api, capi, s1, w1, l1, cam1, 1, threads)
+        res["c1_full"] = {"value": n1 / dt1 / 1e6, "unit": "Msamples/s", "seconds": round(dt1, 3), "samples": n1,
+                          "config": "BASELINE configs[0]: book-1 random spheres 400x225, 100 spp (10^2 traced), depth 50, "
+                                    f"whole frame, {threads} threads"}
+    return res
 
 
-def load_pmc_traffic(path):
-    """HBM bytes per launch of the path kernel from a committed rocprofv3 PMC
-    summary (profiles/), or None."""
+def latest_profile(name):
+    """profiles/rNN/<name> of the newest round that has it, or None."""
+    base = os.path.join(ROOT, "profiles")
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+        rounds = sorted((d for d in os.listdir(base) if d.startswith("r")), reverse=True)
+    except OSError:
         return None
+    for r in rounds:
+        p = os.path.join(base, r, name)
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def load_profile_field(name, field):
+    """One field of a committed rocprofv3 summary (profiles/), or None."""
+    p = latest_profile(name)
+    if not p:
+        return None, None
+    try:
+        with open(p) as f:
+            return json.load(f).get(field), os.path.relpath(p, ROOT)
+    except (OSError, ValueError):
+        return None, None
 
 
 def main():
@@ -127,10 +186,15 @@ def main():
     ap.add_argument("--spp", type=int, default=None, help="default: the config's spp")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-rate", action="store_true", help="skip the host-buffer (PCIe-inclusive) frame")
     ap.add_argument("--reference-bvh", action="store_true",
                     help="A/B only: keep the reference BVH topology instead of the SAH rebuild")
-    ap.add_argument("--backend", default="nccl", help="nccl (= RCCL) on GPU nodes; gloo only to rehearse ranks on one GPU")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl",
+                    help="nccl: ranks gather through the library's RCCL communicator (rt_comm_init); "
+                         "gloo: rehearse ranks on one GPU with a torch gather (harness only)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="one process drives --gpus N devices through rt_render_opts.devices (no torchrun)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this job may use")
     ap.add_argument("--cpu-row-stride", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=None, help="default: 64 (c2), 36 (c4) -> ~10 s of oracle work")
     args = ap.parse_args()
@@ -145,11 +209,14 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus:
+    if world_size != args.gpus and not args.in_process:
         if world_size == 1 and args.gpus > 1:
-            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one process per GPU)",
-                  file=sys.stderr)
+            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one process per GPU), "
+                  "or with --in-process", file=sys.stderr)
             sys.exit(2)
+    if args.in_process and world_size != 1:
+        print("bench.py: --in-process runs as one process", file=sys.stderr)
+        sys.exit(2)
     distributed = world_size > 1
     local_dev = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_dev)
@@ -171,31 +238,51 @@ def main():
     world, lights, cam, desc = build_workload(scenes, scene, args.workload, args.width, args.spp)
     H, W = cam.image_height, cam.image_width
     c = cam.to_c()
-    opts = capi.RtRenderOpts()
-    api.render_opts_default(ctypes.byref(opts))
-    opts.seed = args.seed
-    opts.row_offset = rank
-    opts.row_stride = world_size
-    opts.flags = 1 if args.reference_bvh else 0  # RT_FLAG_REFERENCE_BVH
-    rows = api.shard_rows(ctypes.byref(c), ctypes.byref(opts))
+    lib_gather = distributed and args.backend == "nccl"
+    comm = None
+    if lib_gather:
+        # the frame gather is the library's RCCL group; the id travels over the torch process group
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            api.check(api.comm_unique_id(uid))
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+        comm = api.comm_init(uid, world_size, rank)
+        if not comm:
+            raise RuntimeError("rt_comm_init: " + api.last_error().decode())
+        opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0, comm=comm)
+        rows = H if rank == 0 else 0
+    elif args.in_process:
+        n_dev = args.gpus
+        if n_dev > torch.cuda.device_count():
+            print(f"bench.py: --in-process --gpus {n_dev} but only {torch.cuda.device_count()} devices", file=sys.stderr)
+            sys.exit(2)
+        opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0,
+                                     devices=list(range(n_dev)))
+        rows = H
+    else:
+        # N = 1, or the gloo rehearsal: this rank renders its interleaved rows itself
+        opts, keep = rt.Camera._opts(api, args.seed, rank, world_size, 0, 1 if args.reference_bvh else 0)
+        rows = api.shard_rows(ctypes.byref(c), ctypes.byref(opts))
     out = torch.empty((max(rows, 1), W, 3), dtype=torch.float32, device=device)
     stream = torch.cuda.current_stream(device)
     opts.stream = ctypes.c_void_p(stream.cuda_stream)
     lights_h = -1 if lights is None else lights.h
-    kernel_ms = []
+    kernel_ms, gather_ms = [], []
 
     def step(record):
-        api.check(api.render_device(scene.s, world.h, lights_h, ctypes.byref(c), ctypes.byref(opts),
-                                    ctypes.c_void_p(out.data_ptr())))
+        ptr = ctypes.c_void_p(out.data_ptr()) if rows > 0 else None
+        api.check(api.render_device(scene.s, world.h, lights_h, ctypes.byref(c), ctypes.byref(opts), ptr))
         st = capi.RtStats()
         api.check(api.render_device_wait(scene.s, ctypes.byref(st)))  # HIP events around the path kernel
         if record:
             kernel_ms.append(st.kernel_ms)
+            gather_ms.append(st.gather_ms)
         if rank == 0 and st.kernel_ms > 5000.0:  # long frames (C5 on few GPUs): show progress
             print("bench.py: frame %.1f s" % (st.kernel_ms / 1e3), file=sys.stderr, flush=True)
-        if distributed:
-            shard = out[:rows] if args.backend == "nccl" else out[:rows].cpu()
-            frame = pdist.gather_frame(shard, H, W)
+        if distributed and not lib_gather:
+            frame = pdist.gather_frame(out[:rows].cpu(), H, W)
         else:
             frame = out
         return frame, st
@@ -212,16 +299,12 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kernel_avg_ms = sum(kernel_ms) / len(kernel_ms)
     if distributed:
         rdev = device if args.backend == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+        t = torch.tensor([elapsed, kernel_avg_ms], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        km = torch.tensor([sum(kernel_ms) / len(kernel_ms)], dtype=torch.float64, device=rdev)
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
-        kernel_avg_ms = km.item()
-    else:
-        kernel_avg_ms = sum(kernel_ms) / len(kernel_ms)
+        elapsed, kernel_avg_ms = t[0].item(), t[1].item()
 
     sqrt_spp = cam.sqrt_spp
     frame_samples = W * H * sqrt_spp * sqrt_spp
@@ -230,12 +313,21 @@ def main():
         assert torch.isfinite(frame).all().item()
         wc_path = os.path.join(ROOT, "bench_data", f"work_counts_{args.workload}.json")
         wc = json.load(open(wc_path))
-        # one launch of the path kernel processes this rank's rows
-        launch_samples = W * rows * sqrt_spp * sqrt_spp
+        # one launch of the path kernel processes this rank's (or device's) rows
+        parts = max(world_size, args.gpus if args.in_process else 1)
+        launch_rows = -(-H // parts)
+        launch_samples = W * launch_rows * sqrt_spp * sqrt_spp
         flops = wc["flops_per_sample"] * launch_samples
         achieved = flops / (kernel_avg_ms * 1e-3) / 1e12
-        traffic = (load_pmc_traffic(os.path.join(ROOT, "profiles", "r01", f"pmc_{args.workload}.json"))
-                   if world_size == 1 else None)
+        traffic, traffic_src = (load_profile_field(f"pmc_{args.workload}.json", "hbm_bytes_per_launch")
+                                if parts == 1 else (None, None))
+        exec_fps, exec_src = load_profile_field(f"valu_{args.workload}.json", "executed_f64_flops_per_sample")
+        n = world_size if distributed else (args.gpus if args.in_process else 1)
+        how = ("one frame per step on one GPU" if n == 1 else
+               f"one frame per step, rows interleaved over {n} GPUs, " +
+               ("RCCL gather to rank 0 inside librt_mi355x.so (rt_comm_init)" if lib_gather else
+                "RCCL gather onto device 0 inside librt_mi355x.so (rt_render_opts.devices)" if args.in_process else
+                "torch gather to rank 0 (gloo rehearsal harness)"))
         line = {
             "metric": {"c2": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
                        "c3": "Msamples/s (pixels x traced spp / s), book-2 Cornell box + smoke 800x800, 1024 spp",
@@ -243,7 +335,7 @@ def main():
                        "c5": "Msamples/s (pixels x traced spp / s), book-2 final scene 3840x2160, 4096 spp"}[args.workload],
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world_size,
+            "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -257,10 +349,9 @@ def main():
                      "c5": "the reference's final_scene (main.rs:384-539), randomness from SplitMix64(2025)"}[args.workload]
                     + ", render RNG seed " + str(args.seed),
             "config": {
-                "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth {cam.max_depth}, "
-                            "one frame per step, rows interleaved across ranks, RCCL gather to rank 0",
+                "workload": f"{desc} {W}x{H}, spp {args.spp} ({sqrt_spp**2} traced), max_depth {cam.max_depth}, {how}",
                 "frame_samples": frame_samples,
-                "parallelism": f"row-shard x{world_size}",
+                "parallelism": f"row-shard x{n}",
                 "bvh": "reference topology" if args.reference_bvh else "binned SAH collapsed to 4-wide f32 nodes",
             },
             "roofline": {
@@ -273,14 +364,47 @@ def main():
                 "kernel": "rt_path_kernel",
                 "kernel_ms_avg": round(kernel_avg_ms, 3),
                 "flops_per_sample": round(wc["flops_per_sample"], 1),
-                "note": "algorithmic f64 FLOPs (reference algorithm on the reference BVH topology, "
-                        "bench_data/work_counts_<workload>.json) per launch / path-kernel time (HIP events on the render stream)",
+                "frac_basis": "reference-algorithm work: algorithmic f64 FLOPs of the reference algorithm on the "
+                              "reference BVH topology (bench_data/work_counts_<workload>.json) per launch / path-kernel "
+                              "time (HIP events on the render stream) -- a throughput normalisation, not hardware "
+                              "utilisation; frac_executed is the executed-instruction view",
+                "traffic_source": traffic_src,
             },
         }
-        if world_size == 1 and not args.no_cpu_baseline:
+        if exec_fps:
+            ach_e = exec_fps * launch_samples / (kernel_avg_ms * 1e-3) / 1e12
+            line["roofline"]["achieved_executed"] = round(ach_e, 4)
+            line["roofline"]["frac_executed"] = round(ach_e / FP64_VECTOR_PEAK_TFLOPS, 5)
+            line["roofline"]["executed_source"] = exec_src + " (rocprofv3 SQ_INSTS_VALU_*_F64 x 64 lanes x exec " \
+                                                             "density, per traced sample) x this launch's samples"
+        if n > 1:
+            line["gather_ms_avg"] = round(sum(gather_ms) / len(gather_ms), 3)
+        if world_size == 1 and not args.in_process and not args.no_host_rate:
+            # the PCIe-inclusive rate: rt_render into caller-owned host buffers
+            # (linear f32 + sRGB bytes), SURVEY §8(d)'s t_render
+            hopts, _hk = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0)
+            import numpy as np
+            hl = np.empty((H, W, 3), dtype=np.float32)
+            hs = np.empty((H, W, 3), dtype=np.uint8)
+            hst = capi.RtStats()
+            th = time.perf_counter()
+            api.check(api.render(scene.s, world.h, lights_h, ctypes.byref(c), ctypes.byref(hopts),
+                                 hl.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                 hs.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), ctypes.byref(hst)))
+            dh = time.perf_counter() - th
+            line["host_inclusive"] = {"value": round(frame_samples / dh / 1e6, 3), "unit": "Msamples/s",
+                                      "ms": round(dh * 1e3, 3), "kernel_ms": round(hst.kernel_ms, 3),
+                                      "note": "one rt_render into host buffers (linear f32 + sRGB u8, PCIe copy "
+                                              "included), after the timed steps; not `value`"}
+        if world_size == 1 and not args.in_process and not args.no_cpu_baseline:
             cpu_spp = args.cpu_spp or {"c2": 64, "c3": 400, "c4": 36, "c5": 16}[args.workload]
-            line["cpu_baseline"] = cpu_baseline(args.cpu_threads, args.cpu_row_stride, cpu_spp, args.workload)
+            threads, info = usable_cpus()
+            if args.cpu_threads:
+                threads = args.cpu_threads
+            line["cpu_baseline"] = cpu_baseline(threads, args.cpu_row_stride, cpu_spp, args.workload, info)
         print(json.dumps(line), flush=True)
+    if comm:
+        api.comm_destroy(comm)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum rt_status {
     RT_OK = 0,
@@ -144,13 +144,30 @@ void rt_camera_default(rt_camera* cam);
 /* Camera::initilize's image_height (camera.rs:205-210) */
 uint32_t rt_camera_image_height(const rt_camera* cam);
 
+typedef struct rt_comm rt_comm;
+
 typedef struct rt_render_opts {
     uint64_t seed;       /* render RNG key (oracle/rng_contract.hpp) */
     uint32_t row_offset; /* shard: render rows y = row_offset + k*row_stride */
     uint32_t row_stride; /* 0 or 1 = every row */
     uint32_t threads;    /* CPU implementations only; 0 = all cores */
     uint32_t flags;      /* RT_FLAG_* */
-    void* stream;        /* hipStream_t for rt_render_device; NULL = default */
+    void* stream;        /* hipStream_t for rt_render_device (of devices[0] when n_devices > 1); NULL = default */
+    /* In-process multi-GPU (replaces the rayon pool, camera.rs:178-197):
+     * n_devices > 1 renders the shard's rows interleaved over the HIP devices
+     * devices[0..n_devices) -- part k takes the shard rows k, k + n, k + 2n,
+     * ... -- one host thread per device (world flatten shared, one upload per
+     * device), and gathers the parts onto devices[0] over RCCL (ncclSend /
+     * ncclRecv in one group; peer copies when a device repeats in the list).
+     * 0 or 1 = the calling thread's current device only. */
+    uint32_t n_devices;
+    uint32_t reserved;
+    const int32_t* devices;
+    /* Multi-process (one process per GPU): a communicator from rt_comm_init.
+     * Rank r renders the shard rows r, r + nranks, ... on its current device;
+     * rank 0 receives the whole shard (RCCL gather), other ranks' outputs are
+     * not written.  Exclusive with n_devices > 1. */
+    rt_comm* comm;
 } rt_render_opts;
 
 /* Keep the reference BVH topology (bvh.rs:16-46: longest axis, sort by box
@@ -161,14 +178,14 @@ typedef struct rt_render_opts {
 void rt_render_opts_default(rt_render_opts* opts);
 
 typedef struct rt_stats {
-    uint64_t samples;         /* traced camera samples (pixels x floor(sqrt(spp))^2) */
+    uint64_t samples;         /* traced camera samples (pixels x floor(sqrt(spp))^2), all devices of this call */
     uint64_t rays;            /* ray_color calls that reached world.hit */
     uint64_t panics;          /* reference assert/expect conditions (NaN, zero pdf, ...) */
-    uint64_t reserved0;
+    uint64_t n_devices;       /* devices that rendered (1 per rank with a comm) */
     double render_ms;         /* wall time of the call (host) */
-    double kernel_ms;         /* device time of the path-tracing kernel (HIP events) */
+    double kernel_ms;         /* device time of the path-tracing kernel (HIP events), max over devices */
     double flatten_ms;        /* world flatten + upload, 0 when cached */
-    double reserved1;
+    double gather_ms;         /* device time of the framebuffer gather on devices[0] / rank 0, 0 without one */
 } rt_stats;
 
 /* Camera::render(&world, lights) (camera.rs:161-202).  world: object handle;
@@ -197,12 +214,33 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t ba
 uint32_t rt_shard_rows(const rt_camera* cam, const rt_render_opts* opts);
 
 /* Device-resident variant: out_linear_rgb_device is a gfx950 device pointer
- * (rows x W x 3 f32).  Enqueued on opts->stream and returns without waiting;
- * stats (if given) are filled by rt_render_device_wait. */
+ * (rows x W x 3 f32; on devices[0] when n_devices > 1; may be NULL on comm
+ * ranks other than 0).  Enqueued on opts->stream and returns without waiting;
+ * stats (if given) are filled by rt_render_device_wait.  Renders on one scene
+ * are ordered: a call's device work starts after the previous call's on the
+ * same device has finished (its stream waits on that call's completion
+ * event), because they share the scene's per-device work buffers. */
 int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam,
                          const rt_render_opts* opts, float* out_linear_rgb_device);
-/* Waits for the last rt_render_device on this scene and reports its stats. */
+/* Waits for the last rt_render_device on this scene and reports its stats
+ * (an earlier call's stats are superseded by a later call's). */
 int32_t rt_render_device_wait(rt_scene* s, rt_stats* stats);
+
+/* Test hook (parity tooling, not part of the reference surface): the f64 sum
+ * of each (pixel, stratum row s_i) of the last single-device render on this
+ * scene -- Sum over s_j of ray_color (camera.rs:183-192) before the 1/spp
+ * scale -- laid out [rows x W][sqrt_spp][3].  n_values must equal
+ * rows * W * sqrt_spp * 3.  Waits for the render. */
+int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values);
+
+/* ---- Multi-process communicator (RCCL) -------------------------------------- */
+#define RT_COMM_ID_BYTES 128
+/* ncclGetUniqueId: call on rank 0 and hand the bytes to every rank. */
+int32_t rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+/* ncclCommInitRank on the calling thread's current HIP device; NULL on failure
+ * (rt_last_error). */
+rt_comm* rt_comm_init(const uint8_t id[RT_COMM_ID_BYTES], int32_t nranks, int32_t rank);
+void rt_comm_destroy(rt_comm* comm);
 
 /* ---- Output stage ---------------------------------------------------------- */
 /* Color::to_rgb (utils/color.rs:27-36) of a device-resident linear framebuffer

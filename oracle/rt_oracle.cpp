@@ -548,13 +548,15 @@ void to_rgb(const Color& c, ToonMap tm, uint8_t out[3]) {
 // camera.rs:161-202 -- rayon par_bridge over pixels restated as a dynamic
 // pixel-chunk queue over `threads` std::threads.
 RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, uint64_t seed, int threads,
-                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_offset, uint32_t row_stride) {
+                    std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_offset, uint32_t row_stride,
+                    std::vector<double>* partials) {
     cam.initialize();
     const uint32_t W = cam.image_width, H = cam.image_height;
     if (row_stride < 1) row_stride = 1;
     const uint32_t rows = row_offset >= H ? 0 : (H - row_offset + row_stride - 1) / row_stride;
     linear.assign((size_t)W * rows * 3, 0.0);
     if (srgb) srgb->assign((size_t)W * rows * 3, 0);
+    if (partials) partials->assign((size_t)W * rows * cam.sqrt_spp * 3, 0.0);
     std::atomic<uint64_t> next{0};
     const uint64_t end = (uint64_t)rows * W;
     std::vector<WorkCounts> per_thread(threads > 0 ? threads : 1);
@@ -574,14 +576,24 @@ RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, 
                     uint32_t i = (uint32_t)(k % W), j = row_offset + (uint32_t)(k / W) * row_stride;
                     uint64_t pix = (uint64_t)j * W + i;
                     Color pixel_color;
-                    for (uint32_t s_i = 0; s_i < cam.sqrt_spp; ++s_i)
+                    for (uint32_t s_i = 0; s_i < cam.sqrt_spp; ++s_i) {
+                        Color row_sum;
                         for (uint32_t s_j = 0; s_j < cam.sqrt_spp; ++s_j) {
                             rng.pixel = (uint32_t)pix;
                             rng.sample = s_i * cam.sqrt_spp + s_j;
                             rng.begin_vertex(0);
                             Ray r = cam.get_ray(i, j, s_i, s_j);
-                            pixel_color += cam.ray_color(r, cam.max_depth, world, lights);
+                            const Color c = cam.ray_color(r, cam.max_depth, world, lights);
+                            pixel_color += c;
+                            if (partials) row_sum += c;
                         }
+                        if (partials) {
+                            double* pd = &(*partials)[(k * cam.sqrt_spp + s_i) * 3];
+                            pd[0] = row_sum[0];
+                            pd[1] = row_sum[1];
+                            pd[2] = row_sum[2];
+                        }
+                    }
                     Color pc = pixel_color * cam.pixel_sample_scale;
                     double* dst = &linear[k * 3];
                     dst[0] = pc[0];

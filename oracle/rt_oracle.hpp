@@ -801,8 +801,10 @@ struct RenderResult {
     double seconds = 0.0;
 };
 // Rows y = row_offset + k*row_stride only, written compact (k-th row at k).
+// partials (optional, test tooling): the sum over s_j of ray_color for each
+// (pixel, stratum row s_i), [rows*W][sqrt_spp][3] -- the GPU's per-item sums.
 RenderResult render(Camera& cam, const Hittable& world, const Hittable* lights, uint64_t seed, int threads,
                     std::vector<double>& linear, std::vector<uint8_t>* srgb, uint32_t row_offset = 0,
-                    uint32_t row_stride = 1);
+                    uint32_t row_stride = 1, std::vector<double>* partials = nullptr);
 
 }  // namespace orc

@@ -433,6 +433,44 @@ int32_t orc_render_f64(rt_scene* s, int32_t world, int32_t lights, const rt_came
     return RT_OK;
     GUARD_END
 }
+// Test tooling: the per-(pixel, stratum row) f64 sums (as rt_render_partials_get).
+int32_t orc_render_partials(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,
+                            double* partials, rt_stats* stats) {
+    if (!s || !c || !partials) return fail(RT_EINVAL, "null");
+    int32_t rc;
+    if ((rc = s->check_obj(world)) != RT_OK) return rc;
+    if (lights != -1 && (rc = s->check_obj(lights)) != RT_OK) return rc;
+    if (c->background_tex != -1 && !s->tex_ok(c->background_tex)) return fail(RT_EHANDLE, "unknown background");
+    if (c->image_width == 0 || !(c->aspect_ratio > 0)) return fail(RT_EINVAL, "bad image size");
+    GUARD_BEGIN
+    Camera cam;
+    cam.aspect_ratio = c->aspect_ratio;
+    cam.image_width = c->image_width;
+    cam.samples_per_pixel = c->samples_per_pixel;
+    cam.max_depth = c->max_depth;
+    cam.background = c->background_tex == -1 ? nullptr : s->tex[c->background_tex];
+    cam.vertical_fov_in_degrees = c->vertical_fov_in_degrees;
+    cam.look_from = v3(c->look_from);
+    cam.look_at = v3(c->look_at);
+    cam.vec_up = v3(c->vec_up);
+    cam.defocus_angle_in_degrees = c->defocus_angle_in_degrees;
+    cam.focus_distance = c->focus_distance;
+    int threads = (o && o->threads) ? (int)o->threads : (int)std::thread::hardware_concurrency();
+    if (threads < 1) threads = 1;
+    std::vector<double> lin, part;
+    RenderResult res = render(cam, *s->obj[world], lights == -1 ? nullptr : s->obj[lights].get(), o ? o->seed : 1,
+                              threads, lin, nullptr, o ? o->row_offset : 0,
+                              (o && o->row_stride > 1) ? o->row_stride : 1, &part);
+    if (!part.empty()) std::memcpy(partials, part.data(), part.size() * sizeof(double));
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        stats->samples = (uint64_t)res.rows * res.width * (uint64_t)cam.sqrt_spp * cam.sqrt_spp;
+        stats->rays = res.counts.ray_color_calls;
+        stats->render_ms = res.seconds * 1e3;
+    }
+    return RT_OK;
+    GUARD_END
+}
 uint32_t orc_work_count_fields(void) { return sizeof(WorkCounts) / sizeof(uint64_t); }
 
 int32_t orc_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* c, const rt_render_opts* o,

@@ -51,6 +51,10 @@ class RtRenderOpts(C.Structure):
         ("threads", C.c_uint32),
         ("flags", C.c_uint32),
         ("stream", C.c_void_p),
+        ("n_devices", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("devices", C.POINTER(C.c_int32)),
+        ("comm", C.c_void_p),
     ]
 
 
@@ -59,11 +63,11 @@ class RtStats(C.Structure):
         ("samples", C.c_uint64),
         ("rays", C.c_uint64),
         ("panics", C.c_uint64),
-        ("reserved0", C.c_uint64),
+        ("n_devices", C.c_uint64),
         ("render_ms", C.c_double),
         ("kernel_ms", C.c_double),
         ("flatten_ms", C.c_double),
-        ("reserved1", C.c_double),
+        ("gather_ms", C.c_double),
     ]
 
 
@@ -117,10 +121,20 @@ SIGNATURES = {
     "write_png": (_I, [C.c_char_p, C.c_uint32, C.c_uint32, _P]),
     "camera_from_json": (_I, [C.c_char_p, C.POINTER(RtCamera)]),
     "world_info_get": (_I, [_P, _I, _I, _I, _U, C.POINTER(RtWorldInfo)]),
+    "render_partials_get": (_I, [_P, _DP, C.c_uint64]),
+    "comm_unique_id": (_I, [C.POINTER(C.c_uint8)]),
+    "comm_init": (_P, [C.POINTER(C.c_uint8), _I, _I]),
+    "comm_destroy": (None, [_P]),
 }
+
+# Entry points of the GPU library only (the oracle renders on host cores and
+# has no communicator or device-side partial sums).
+GPU_ONLY = ("render_partials_get", "comm_unique_id", "comm_init", "comm_destroy")
 
 # Entry points only a CPU implementation has (the oracle).
 ORACLE_EXTRAS = {
+    # the f64 per-(pixel, stratum row) sums, [rows x W][sqrt_spp][3] (as rt_render_partials_get)
+    "render_partials": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _DP, C.POINTER(RtStats)]),
     "render_f64": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _DP, C.POINTER(C.c_uint8),
                         C.POINTER(RtStats), C.POINTER(C.c_uint64)]),
     "work_count_fields": (_U, []),

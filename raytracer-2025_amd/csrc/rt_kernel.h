@@ -75,6 +75,11 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
                                        double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
                                        int toon, hipStream_t stream, int tier, int grid, void* params_dev,
                                        void* stack_ovf);
+// Re-interleaves a gathered frame: staging holds `parts` slices of `slice`
+// floats, slice k = the compact rows k, k + parts, ... of the frame; out gets
+// the frame's `rows` compact rows (rows x W x 3 f32).
+extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice, float* out, uint32_t rows, uint32_t W,
+                                              uint32_t parts, hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream);
 // device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);

@@ -1673,6 +1673,18 @@ __global__ void __launch_bounds__(256) rt_to_rgb_kernel(const float* __restrict_
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) srgb[i] = srgb_u8((double)lin[i], toon);
 }
+// Frame row j of a gathered shard came from part j % parts, as that part's
+// compact row j / parts.  One thread per float of the frame.
+__global__ void __launch_bounds__(256) rt_deinterleave_kernel(const float* __restrict__ staging, uint64_t slice,
+                                                              float* __restrict__ out, uint32_t rows, uint32_t W,
+                                                              uint32_t parts) {
+    const uint64_t row_floats = (uint64_t)W * 3;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)rows * row_floats) return;
+    const uint32_t j = (uint32_t)(i / row_floats);
+    const uint64_t x = i - (uint64_t)j * row_floats;
+    out[i] = staging[(uint64_t)(j % parts) * slice + (uint64_t)(j / parts) * row_floats + x];
+}
 }  // namespace rtk
 
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
@@ -1736,6 +1748,15 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
                        fd->pixel_sample_scale, out, srgb, toon);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice, float* out, uint32_t rows, uint32_t W,
+                                              uint32_t parts, hipStream_t stream) {
+    const uint64_t n = (uint64_t)rows * W * 3;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rtk::rt_deinterleave_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, staging,
+                       (uint64_t)slice, out, rows, W, parts);
     return hipGetLastError();
 }
 

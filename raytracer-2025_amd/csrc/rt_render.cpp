@@ -1,51 +1,160 @@
 // rt_render.cpp -- render half of the C ABI: Camera::initilize on the host,
-// world upload (one device blob per scene, cached until the scene changes),
-// and the blocking / stream-ordered render entry points.
+// world upload (one device blob per scene and device, cached until the scene
+// changes), the blocking / stream-ordered render entry points, and the
+// multi-GPU row split with its one framebuffer gather (RCCL over xGMI).
+//
+// The reference renders with rayon over pixels (camera.rs:178-197).  Here a
+// render is split into parts, one per device: part k of n takes the shard's
+// rows k, k + n, ... (row interleave, so sky and ground rows balance) and
+// renders them with the persistent path kernel of its device.  With n > 1 the
+// parts' compact rows are gathered onto the root device (devices[0], or comm
+// rank 0) by ncclSend / ncclRecv in one group and re-interleaved there by one
+// small kernel -- the only exchange of the frame.
+#include <dlfcn.h>
+
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <thread>
+
+#include <rccl/rccl.h>
 
 #include "../../include/rt_mi355x.h"
 #include "rt_kernel.h"
 #include "rt_scene.hpp"
 
+// ---------------------------------------------------------------------------- RCCL
+// librccl is opened on first use (a single-GPU render never loads it).
+namespace {
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+RcclApi& rccl() {
+    static RcclApi a;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            a.err = std::string("cannot load librccl: ") + (e ? e : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn) {
+                all = false;
+                a.err = std::string("librccl lacks ") + name;
+            }
+        };
+        sym(a.get_unique_id, "ncclGetUniqueId");
+        sym(a.comm_init_rank, "ncclCommInitRank");
+        sym(a.comm_init_all, "ncclCommInitAll");
+        sym(a.comm_destroy, "ncclCommDestroy");
+        sym(a.send, "ncclSend");
+        sym(a.recv, "ncclRecv");
+        sym(a.group_start, "ncclGroupStart");
+        sym(a.group_end, "ncclGroupEnd");
+        sym(a.error_string, "ncclGetErrorString");
+        a.ok = all;
+    });
+    return a;
+}
+}  // namespace
+
+struct rt_comm {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = -1;
+};
+
 namespace rth {
+
+// The calling thread's current device, restored on scope exit: the library
+// switches devices for the parts and the gather but leaves the caller's as it was.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
 
 struct DeviceWorld {
     int device = -1;
     int32_t world = -1, lights = -1, background = -1;
     uint64_t generation = ~0ull;
+    bool reference_bvh = false;
     char* blob = nullptr;
     size_t blob_bytes = 0;
     rtk::SceneView view{};
-    size_t n_prims = 0;
+    int tier = 1;
+    int grid[rtk::N_TIERS] = {};
+    int cus = 0;
     // frame work buffers (grow-only)
     uint32_t* queue = nullptr;
     unsigned long long* stats = nullptr;
     void* params = nullptr;
     double* partial = nullptr;
     size_t partial_bytes = 0;
-    float* out = nullptr;
+    float* out = nullptr;  // the part's compact rows when they are not written to the caller's buffer
     size_t out_bytes = 0;
     uint8_t* srgb = nullptr;  // to_rgb bytes of the host-path render
     size_t srgb_bytes = 0;
-    void* stack_ovf = nullptr;  // mesh tier: traversal-stack entries beyond the LDS part
+    void* stack_ovf = nullptr;  // mesh / full tiers: traversal-stack entries beyond the LDS part
     size_t stack_ovf_bytes = 0;
+    hipStream_t own_stream = nullptr;  // for parts that do not run on the caller's stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-    // last async render
-    bool pending = false;
-    uint64_t pending_samples = 0;
-    double pending_flatten_ms = 0;
-    std::chrono::steady_clock::time_point pending_t0;
-    int grid[rtk::N_TIERS] = {};
-    int tier = 1;
-    int cus = 0;
-    bool reference_bvh = false;
-    hipStream_t pending_stream = nullptr;
+    hipEvent_t ev_done = nullptr;  // after the slot's last device work (orders the next render)
+    bool done_recorded = false;
+    // the last render on this slot
+    bool ran = false;  // the path kernel ran (ev_start / ev_stop are valid)
+    uint64_t samples = 0;
+    uint32_t W = 0, rows = 0, S = 0;
+    hipStream_t last_stream = nullptr;
 };
 
-void destroy_device_world(DeviceWorld* d) {
+struct RenderState {
+    std::vector<DeviceWorld*> slots;  // slot k renders part k; slot 0 also serves single-device renders
+    // gather buffers on the root device
+    int root_device = -1;
+    float* staging = nullptr;
+    size_t staging_bytes = 0;
+    float* full = nullptr;  // gathered frame of a host-buffer render
+    size_t full_bytes = 0;
+    uint8_t* full_srgb = nullptr;
+    size_t full_srgb_bytes = 0;
+    hipEvent_t g_start = nullptr, g_stop = nullptr;
+    bool g_recorded = false;
+    // ncclCommInitAll communicators of the last device list with distinct devices
+    std::vector<int> comm_devices;
+    std::vector<ncclComm_t> comms;
+    // the last render
+    int n_parts = 0;
+    bool gathered = false;
+    bool pending = false;
+    bool is_root = true;
+    hipStream_t root_stream = nullptr;
+    double flatten_ms = 0;
+    std::chrono::steady_clock::time_point t0;
+};
+
+static void destroy_device_world(DeviceWorld* d) {
     if (!d) return;
+    if (d->device >= 0) (void)hipSetDevice(d->device);
+    if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
     if (d->blob) (void)hipFree(d->blob);
     if (d->queue) (void)hipFree(d->queue);
     if (d->stats) (void)hipFree(d->stats);
@@ -56,7 +165,41 @@ void destroy_device_world(DeviceWorld* d) {
     if (d->srgb) (void)hipFree(d->srgb);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
+    if (d->ev_done) (void)hipEventDestroy(d->ev_done);
+    if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
     delete d;
+}
+
+static void free_root_buffers(RenderState* r) {
+    if (r->root_device >= 0) (void)hipSetDevice(r->root_device);
+    if (r->staging) (void)hipFree(r->staging);
+    if (r->full) (void)hipFree(r->full);
+    if (r->full_srgb) (void)hipFree(r->full_srgb);
+    if (r->g_start) (void)hipEventDestroy(r->g_start);
+    if (r->g_stop) (void)hipEventDestroy(r->g_stop);
+    r->staging = r->full = nullptr;
+    r->full_srgb = nullptr;
+    r->staging_bytes = r->full_bytes = r->full_srgb_bytes = 0;
+    r->g_start = r->g_stop = nullptr;
+    r->g_recorded = false;
+    r->root_device = -1;
+}
+
+static void destroy_comms(RenderState* r) {
+    if (!r->comms.empty() && rccl().ok)
+        for (ncclComm_t c : r->comms) (void)rccl().comm_destroy(c);
+    r->comms.clear();
+    r->comm_devices.clear();
+}
+
+void destroy_render_state(RenderState* r) {
+    if (!r) return;
+    DeviceGuard g;
+    (void)hipDeviceSynchronize();
+    destroy_comms(r);
+    for (DeviceWorld* d : r->slots) destroy_device_world(d);
+    free_root_buffers(r);
+    delete r;
 }
 
 // The kernel tier for a flattened world, with the tier's node format applied:
@@ -98,56 +241,137 @@ static size_t put(std::vector<char>& blob, const std::vector<T>& v) {
     return off;
 }
 
-// Checks there is a gfx950 device and binds the scene's device world to it,
-// flattening + uploading when (world, lights, background, scene) changed.
-static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, bool reference_bvh, double& flatten_ms) {
-    flatten_ms = 0;
-    int dev = -1;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return hip_fail(e, "hipGetDevice (no HIP device)");
+// The world of one render flattened once on the host and shared by every
+// device that needs an upload (built by the first part that needs it).
+struct FlatWorld {
+    std::mutex m;
+    bool done = false;
+    int32_t rc = RT_OK;
+    std::string err;
+    double ms = 0;
+    int tier = 1;
+    uint32_t stack_need = 0;
+    std::vector<char> blob;
+    rtk::SceneView rel{};  // SceneView with byte offsets into blob instead of pointers
+    size_t n_prims = 0;
+};
+
+static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg, bool reference_bvh, FlatWorld& fw) {
+    std::lock_guard<std::mutex> lk(fw.m);
+    if (fw.done) {
+        if (fw.rc != RT_OK) set_error(fw.rc, fw.err);
+        return fw.rc;
+    }
+    fw.done = true;
+    auto t0 = std::chrono::steady_clock::now();
+    HostWorld hw;
+    int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
+    int tier = rc == RT_OK ? prepare_tier(hw) : -1;
+    if (rc == RT_OK && tier < 0) rc = RT_ESTACK;
+    if (rc == RT_OK) {
+        const uint32_t stack_cap = rtk_stack_entries(tier);
+        if (hw.stack_need > stack_cap)
+            rc = set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) +
+                                          " traversal-stack entries, kernel has " + std::to_string(stack_cap));
+    }
+    if (rc != RT_OK) {
+        fw.rc = rc;
+        fw.err = rt_last_error();
+        return rc;
+    }
+    std::vector<char>& blob = fw.blob;
+    auto off = [](size_t o) { return (uintptr_t)o; };
+    rtk::SceneView& v = fw.rel;
+    v.nodes = (const rtk::DNode*)off(put(blob, hw.nodes));
+    v.nodes4 = (const rtk::DNode4*)off(put(blob, hw.nodes4));
+    v.spheres = (const double4*)off(put(blob, hw.spheres));
+    v.sphere_mat = (const int32_t*)off(put(blob, hw.sphere_mat));
+    v.msph_center = (const double4*)off(put(blob, hw.msph_center));
+    v.msph_dir = (const double4*)off(put(blob, hw.msph_dir));
+    v.msph_mat = (const int32_t*)off(put(blob, hw.msph_mat));
+    v.planars = (const rtk::DPlanar*)off(put(blob, hw.planars));
+    v.planar_area = (const double*)off(put(blob, hw.planar_area));
+    v.planar_mat = (const int32_t*)off(put(blob, hw.planar_mat));
+    v.planar_remap = (const int32_t*)off(put(blob, hw.planar_remap));
+    v.remaps = (const rtk::DRemap*)off(put(blob, hw.remaps));
+    v.remap_nm = (const rtk::DRemapNM*)off(
+        put(blob, (hw.features & rtk::F_NORMALMAP) ? hw.remap_nm : std::vector<rtk::DRemapNM>()));
+    v.list_children = (const uint32_t*)off(put(blob, hw.list_children));
+    v.xforms = (const rtk::DXform*)off(put(blob, hw.xforms));
+    v.media = (const rtk::DMedium*)off(put(blob, hw.media));
+    v.materials = (const rtk::DMaterial*)off(put(blob, hw.materials));
+    v.textures = (const rtk::DTexture*)off(put(blob, hw.textures));
+    v.texels = (const float*)off(put(blob, hw.texels));
+    v.perlin = (const rtk::DPerlin*)off(put(blob, hw.perlin));
+    v.world_root = hw.world_root;
+    v.lights_root = hw.lights_root;
+    v.background_tex = bg;
+    v.stack_need = hw.stack_need;
+    v.features = hw.features;
+    v.n_nodes4 = (uint32_t)hw.nodes4.size();
+    fw.tier = tier;
+    fw.stack_need = hw.stack_need;
+    fw.n_prims = hw.n_prims;
+    fw.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return RT_OK;
+}
+
+// A slot's device world on `device` (the thread's current device), created on
+// first use (work buffers, events, stream, the grid of each tier).
+static int32_t slot_for(RenderState* r, size_t k, int device, DeviceWorld*& out) {
+    DeviceWorld* d = r->slots[k];
+    if (d && d->device != device) {
+        destroy_device_world(d);
+        r->slots[k] = d = nullptr;
+        (void)hipSetDevice(device);
+    }
+    if (d) {
+        out = d;
+        return RT_OK;
+    }
     hipDeviceProp_t prop;
-    e = hipGetDeviceProperties(&prop, dev);
+    hipError_t e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return set_error(RT_EDEVICE, std::string("librt_mi355x.so needs a gfx950 device, found ") + prop.gcnArchName);
-    DeviceWorld* d = s->dev;
-    if (d && d->device != dev) {
-        destroy_device_world(d);
-        s->dev = d = nullptr;
+    d = new DeviceWorld();
+    d->device = device;
+    r->slots[k] = d;
+    if ((e = hipMalloc(&d->queue, 256)) != hipSuccess) return hip_fail(e, "hipMalloc queue");
+    if ((e = hipMalloc(&d->stats, 256)) != hipSuccess) return hip_fail(e, "hipMalloc stats");
+    if ((e = hipMalloc(&d->params, rtk_params_bytes())) != hipSuccess) return hip_fail(e, "hipMalloc params");
+    if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "hipEventCreate");
+    if ((e = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "hipStreamCreate");
+    for (int t = 0; t < rtk::N_TIERS; ++t) {
+        int bpc = 0;
+        if ((e = (hipError_t)rtk_path_kernel_occupancy(t, &bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
+        if (bpc < 1) bpc = 1;
+        d->grid[t] = bpc * prop.multiProcessorCount;
     }
-    if (!d) {
-        d = new DeviceWorld();
-        d->device = dev;
-        s->dev = d;
-        if ((e = hipMalloc(&d->queue, 256)) != hipSuccess) return hip_fail(e, "hipMalloc queue");
-        if ((e = hipMalloc(&d->stats, 256)) != hipSuccess) return hip_fail(e, "hipMalloc stats");
-        if ((e = hipMalloc(&d->params, rtk_params_bytes())) != hipSuccess) return hip_fail(e, "hipMalloc params");
-        if ((e = hipEventCreate(&d->ev_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        if ((e = hipEventCreate(&d->ev_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        for (int t = 0; t < rtk::N_TIERS; ++t) {
-            int bpc = 0;
-            if ((e = (hipError_t)rtk_path_kernel_occupancy(t, &bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
-            if (bpc < 1) bpc = 1;
-            d->grid[t] = bpc * prop.multiProcessorCount;
-        }
-        d->cus = prop.multiProcessorCount;
-    }
+    d->cus = prop.multiProcessorCount;
+    out = d;
+    return RT_OK;
+}
+
+// Uploads the world to the slot's device unless it already holds this
+// (world, lights, background, scene generation, topology).
+static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t lights, int32_t bg, bool reference_bvh,
+                            FlatWorld& fw, double& flatten_ms) {
+    flatten_ms = 0;
     if (d->blob && d->world == world && d->lights == lights && d->background == bg && d->generation == s->generation &&
         d->reference_bvh == reference_bvh)
         return RT_OK;
     auto t0 = std::chrono::steady_clock::now();
-    HostWorld hw;
-    int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
+    int32_t rc = build_flat(s, world, lights, bg, reference_bvh, fw);
     if (rc != RT_OK) return rc;
-    const int tier = prepare_tier(hw);
-    if (tier < 0) return RT_ESTACK;
-    const uint32_t stack_cap = rtk_stack_entries(tier);
-    if (hw.stack_need > stack_cap)
-        return set_error(RT_ESTACK, "world needs " + std::to_string(hw.stack_need) + " traversal-stack entries, kernel has " +
-                                        std::to_string(stack_cap));
-    const uint32_t lds_entries = rtk::lds_stack_entries(tier);
-    if (hw.stack_need > lds_entries) {
-        const size_t need = (size_t)(hw.stack_need - lds_entries) * d->grid[tier] * RT_BLOCK * sizeof(uint64_t);
+    hipError_t e;
+    const uint32_t lds_entries = rtk::lds_stack_entries(fw.tier);
+    if (fw.stack_need > lds_entries) {
+        const size_t need = (size_t)(fw.stack_need - lds_entries) * d->grid[fw.tier] * RT_BLOCK * sizeof(uint64_t);
         if (need > d->stack_ovf_bytes) {
             if (d->stack_ovf) (void)hipFree(d->stack_ovf);
             d->stack_ovf = nullptr;
@@ -156,54 +380,25 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
             d->stack_ovf_bytes = need;
         }
     }
-    std::vector<char> blob;
-    size_t o_nodes = put(blob, hw.nodes), o_n4 = put(blob, hw.nodes4), o_sph = put(blob, hw.spheres), o_sphm = put(blob, hw.sphere_mat),
-           o_msc = put(blob, hw.msph_center), o_msd = put(blob, hw.msph_dir), o_msm = put(blob, hw.msph_mat),
-           o_pl = put(blob, hw.planars), o_pla = put(blob, hw.planar_area), o_plm = put(blob, hw.planar_mat),
-           o_plr = put(blob, hw.planar_remap), o_rm = put(blob, hw.remaps),
-           o_rnm = put(blob, (hw.features & rtk::F_NORMALMAP) ? hw.remap_nm : std::vector<rtk::DRemapNM>()),
-           o_lc = put(blob, hw.list_children), o_xf = put(blob, hw.xforms), o_md = put(blob, hw.media),
-           o_mat = put(blob, hw.materials), o_tex = put(blob, hw.textures), o_tx = put(blob, hw.texels),
-           o_per = put(blob, hw.perlin);
     if (d->blob) {
         (void)hipFree(d->blob);
         d->blob = nullptr;
     }
-    if ((e = hipMalloc(&d->blob, blob.size() + 256)) != hipSuccess) return hip_fail(e, "hipMalloc world");
-    if ((e = hipMemcpy(d->blob, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
+    d->world = -1;  // invalid until the upload completes
+    if ((e = hipMalloc(&d->blob, fw.blob.size() + 256)) != hipSuccess) return hip_fail(e, "hipMalloc world");
+    if ((e = hipMemcpy(d->blob, fw.blob.data(), fw.blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "hipMemcpy world");
     char* b = d->blob;
-    rtk::SceneView& v = d->view;
-    v.nodes = (const rtk::DNode*)(b + o_nodes);
-    v.nodes4 = (const rtk::DNode4*)(b + o_n4);
-    v.spheres = (const double4*)(b + o_sph);
-    v.sphere_mat = (const int32_t*)(b + o_sphm);
-    v.msph_center = (const double4*)(b + o_msc);
-    v.msph_dir = (const double4*)(b + o_msd);
-    v.msph_mat = (const int32_t*)(b + o_msm);
-    v.planars = (const rtk::DPlanar*)(b + o_pl);
-    v.planar_area = (const double*)(b + o_pla);
-    v.planar_mat = (const int32_t*)(b + o_plm);
-    v.planar_remap = (const int32_t*)(b + o_plr);
-    v.remaps = (const rtk::DRemap*)(b + o_rm);
-    v.remap_nm = (const rtk::DRemapNM*)(b + o_rnm);
-    v.list_children = (const uint32_t*)(b + o_lc);
-    v.xforms = (const rtk::DXform*)(b + o_xf);
-    v.media = (const rtk::DMedium*)(b + o_md);
-    v.materials = (const rtk::DMaterial*)(b + o_mat);
-    v.textures = (const rtk::DTexture*)(b + o_tex);
-    v.texels = (const float*)(b + o_tx);
-    v.perlin = (const rtk::DPerlin*)(b + o_per);
-    v.world_root = hw.world_root;
-    v.lights_root = hw.lights_root;
-    v.background_tex = bg;
-    v.stack_need = hw.stack_need;
-    v.features = hw.features;
-    v.n_nodes4 = (uint32_t)hw.nodes4.size();
-    d->tier = tier;
+    rtk::SceneView v = fw.rel;
+    auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
+    fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
+        fix(v.msph_mat), fix(v.planars), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
+        fix(v.remap_nm), fix(v.list_children), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
+        fix(v.texels), fix(v.perlin);
+    d->view = v;
+    d->tier = fw.tier;
     d->reference_bvh = reference_bvh;
-    d->blob_bytes = blob.size();
-    d->n_prims = hw.n_prims;
+    d->blob_bytes = fw.blob.size();
     d->world = world;
     d->lights = lights;
     d->background = bg;
@@ -212,20 +407,21 @@ static int32_t prepare(rt_scene* s, int32_t world, int32_t lights, int32_t bg, b
     return RT_OK;
 }
 
-// Camera::initilize (camera.rs:204-245)
-static int32_t init_frame(const rt_camera* c, const rt_render_opts* o, rtk_frame_desc& f) {
+// Camera::initilize (camera.rs:204-245) for the rows y = row_offset + k * row_stride
+static int32_t init_frame(const rt_camera* c, uint64_t seed, uint32_t row_offset, uint32_t row_stride,
+                          rtk_frame_desc& f) {
     if (!c) return set_error(RT_EINVAL, "null camera");
     if (c->image_width == 0 || !(c->aspect_ratio > 0)) return set_error(RT_EINVAL, "bad image size");
     const double PI = 3.14159265358979323846;
     const uint32_t W = c->image_width, H = rt_camera_image_height(c);
     std::memset(&f, 0, sizeof f);
     f.W = W;
-    f.row_stride = (o && o->row_stride > 1) ? o->row_stride : 1;
-    f.row_offset = o ? o->row_offset : 0;
-    f.rows = rt_shard_rows(c, o);
+    f.row_stride = row_stride > 1 ? row_stride : 1;
+    f.row_offset = row_offset;
+    f.rows = row_offset >= H ? 0 : (H - row_offset + f.row_stride - 1) / f.row_stride;
     f.S = (uint32_t)std::sqrt((double)c->samples_per_pixel);
     f.max_depth = c->max_depth;
-    f.seed = o ? o->seed : 1;
+    f.seed = seed;
     f.pixel_sample_scale = 1.0 / (double)(f.S * f.S);
     f.recip_sqrt_spp = 1.0 / (double)f.S;
     if ((uint64_t)W * f.rows * f.S >= 0xFFF00000ull) return set_error(RT_EINVAL, "frame too large for one launch");
@@ -261,30 +457,127 @@ static int32_t init_frame(const rt_camera* c, const rt_render_opts* o, rtk_frame
     return RT_OK;
 }
 
-static int32_t ensure_buffers(DeviceWorld* d, const rtk_frame_desc& f, bool need_out) {
-    hipError_t e;
-    size_t pb = (size_t)f.W * f.rows * f.S * 3 * sizeof(double);
-    if (pb > d->partial_bytes) {
-        if (d->partial) (void)hipFree(d->partial);
-        d->partial = nullptr;
-        d->partial_bytes = 0;
-        if ((e = hipMalloc(&d->partial, pb)) != hipSuccess) return hip_fail(e, "hipMalloc partial sums");
-        d->partial_bytes = pb;
-    }
-    size_t ob = (size_t)f.W * f.rows * 3 * sizeof(float);
-    if (need_out && ob > d->out_bytes) {
-        if (d->out) (void)hipFree(d->out);
-        d->out = nullptr;
-        d->out_bytes = 0;
-        if ((e = hipMalloc(&d->out, ob)) != hipSuccess) return hip_fail(e, "hipMalloc output");
-        d->out_bytes = ob;
-    }
+static int32_t grow(void** p, size_t& have, size_t need, const char* what) {
+    if (need <= have) return RT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    have = 0;
+    hipError_t e = hipMalloc(p, need);
+    if (e != hipSuccess) return hip_fail(e, what);
+    have = need;
     return RT_OK;
 }
 
-static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
-                      float* dev_out, hipStream_t stream, bool want_srgb = false) {
+// One part of a render: rows row_offset + k * row_stride on one device.
+struct Part {
+    size_t slot = 0;
+    int device = -1;
+    uint32_t row_offset = 0, row_stride = 1;
+    bool user_stream = false;  // part 0 runs on the caller's stream (NULL = the default stream)
+    hipStream_t stream = nullptr;
+    float* out = nullptr;  // nullptr: the slot's own buffer
+    bool want_srgb = false;
+    // results
+    DeviceWorld* d = nullptr;
+    float* out_used = nullptr;
+    uint32_t rows = 0;
+    int32_t rc = RT_OK;
+    std::string err;
+    double flatten_ms = 0;
+};
+
+// Runs on the part's host thread: device world, buffers, kernel launch.
+static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights, const rt_camera* cam, uint64_t seed,
+                     bool reference_bvh, FlatWorld& fw, Part& p) {
+    auto fail = [&](int32_t rc) {
+        p.rc = rc;
+        p.err = rt_last_error();
+    };
+    hipError_t e = hipSetDevice(p.device);
+    if (e != hipSuccess) return fail(hip_fail(e, "hipSetDevice"));
+    int32_t rc = slot_for(r, p.slot, p.device, p.d);
+    if (rc != RT_OK) return fail(rc);
+    DeviceWorld* d = p.d;
+    if (!p.user_stream) p.stream = d->own_stream;
+    if ((rc = upload_world(s, d, world, lights, cam->background_tex, reference_bvh, fw, p.flatten_ms)) != RT_OK)
+        return fail(rc);
+    rtk_frame_desc f;
+    if ((rc = init_frame(cam, seed, p.row_offset, p.row_stride, f)) != RT_OK) return fail(rc);
+    p.rows = f.rows;
+    if ((rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * 3 * sizeof(double),
+                   "hipMalloc partial sums")) != RT_OK)
+        return fail(rc);
+    if (!p.out &&
+        (rc = grow((void**)&d->out, d->out_bytes, (size_t)f.W * f.rows * 3 * sizeof(float), "hipMalloc output")) != RT_OK)
+        return fail(rc);
+    uint8_t* srgb = nullptr;
+    if (p.want_srgb) {
+        if ((rc = grow((void**)&d->srgb, d->srgb_bytes, (size_t)f.W * f.rows * 3, "hipMalloc srgb")) != RT_OK)
+            return fail(rc);
+        srgb = d->srgb;
+    }
+    // order after the previous render's use of this slot's buffers, and after
+    // the gather that read them
+    if (d->done_recorded && (e = hipStreamWaitEvent(p.stream, d->ev_done, 0)) != hipSuccess)
+        return fail(hip_fail(e, "hipStreamWaitEvent"));
+    if (r->g_recorded && (e = hipStreamWaitEvent(p.stream, r->g_stop, 0)) != hipSuccess)
+        return fail(hip_fail(e, "hipStreamWaitEvent"));
+    if ((e = hipMemsetAsync(d->stats, 0, 2 * sizeof(unsigned long long), p.stream)) != hipSuccess)
+        return fail(hip_fail(e, "hipMemsetAsync stats"));
+    f.ev_start = d->ev_start;
+    f.ev_stop = d->ev_stop;
+    float* out = p.out ? p.out : d->out;
+    p.out_used = out;
+    const bool run = f.rows > 0 && f.max_depth > 0;
+    if (run) {
+        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, p.stream, d->tier,
+                             d->grid[d->tier], d->params, d->stack_ovf);
+        if (e != hipSuccess) return fail(hip_fail(e, "kernel launch"));
+    } else if (f.rows > 0) {
+        // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)
+        if ((e = hipMemsetAsync(out, 0, (size_t)f.W * f.rows * 3 * sizeof(float), p.stream)) != hipSuccess)
+            return fail(hip_fail(e, "hipMemsetAsync output"));
+        if (srgb && (e = hipMemsetAsync(srgb, 0, (size_t)f.W * f.rows * 3, p.stream)) != hipSuccess)
+            return fail(hip_fail(e, "hipMemsetAsync srgb"));
+    }
+    if ((e = hipEventRecord(d->ev_done, p.stream)) != hipSuccess) return fail(hip_fail(e, "hipEventRecord"));
+    d->done_recorded = true;
+    d->ran = run;
+    d->samples = (uint64_t)f.W * f.rows * f.S * f.S;
+    d->W = f.W;
+    d->rows = f.rows;
+    d->S = f.S;
+    d->last_stream = p.stream;
+}
+
+static int32_t nccl_fail(ncclResult_t e, const char* what) {
+    return set_error(RT_EDEVICE, std::string(what) + ": " + rccl().error_string(e));
+}
+
+// Root-side buffers of a gather on the current (root) device.
+static int32_t root_buffers(RenderState* r, int device, size_t staging_bytes, size_t full_bytes, size_t srgb_bytes) {
+    if (r->root_device != device) {
+        free_root_buffers(r);
+        (void)hipSetDevice(device);
+        r->root_device = device;
+    }
+    hipError_t e;
+    if (!r->g_start && (e = hipEventCreate(&r->g_start)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    if (!r->g_stop && (e = hipEventCreate(&r->g_stop)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    int32_t rc;
+    if ((rc = grow((void**)&r->staging, r->staging_bytes, staging_bytes, "hipMalloc gather staging")) != RT_OK) return rc;
+    if ((rc = grow((void**)&r->full, r->full_bytes, full_bytes, "hipMalloc gathered frame")) != RT_OK) return rc;
+    if ((rc = grow((void**)&r->full_srgb, r->full_srgb_bytes, srgb_bytes, "hipMalloc gathered srgb")) != RT_OK)
+        return rc;
+    return RT_OK;
+}
+
+// Rows of part k of n of a shard with `rows` compact rows (rows k, k+n, ...).
+static inline uint32_t part_rows(uint32_t rows, uint32_t k, uint32_t n) { return k >= rows ? 0 : (rows - k + n - 1) / n; }
+
+static int32_t validate(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam) {
     if (!s) return set_error(RT_EINVAL, "null scene");
+    if (!cam) return set_error(RT_EINVAL, "null camera");
     if (world < 0 || (size_t)world >= s->objs.size() || s->objs[world].hidden)
         return set_error(RT_EHANDLE, "unknown world handle");
     if (s->objs[world].moved) return set_error(RT_EMOVED, "world handle was moved");
@@ -293,72 +586,203 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
             return set_error(RT_EHANDLE, "unknown lights handle");
         if (s->objs[lights].moved) return set_error(RT_EMOVED, "lights handle was moved");
     }
-    rtk_frame_desc f;
-    int32_t rc = init_frame(cam, opts, f);
-    if (rc != RT_OK) return rc;
     if (cam->background_tex != -1 && (cam->background_tex < 0 || (size_t)cam->background_tex >= s->texs.size()))
         return set_error(RT_EHANDLE, "unknown background texture");
-    double flatten_ms = 0;
+    return RT_OK;
+}
+
+// Enqueues one render (all parts, and the gather when there is more than one
+// part).  dev_out: the caller's device buffer (root), or nullptr for the
+// library's own (rt_render).  On return the render's state is in s->rs.
+static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
+                      float* dev_out, bool host_call, bool want_srgb) {
+    int32_t rc = validate(s, world, lights, cam);
+    if (rc != RT_OK) return rc;
+    const uint64_t seed = opts ? opts->seed : 1;
+    const uint32_t off = opts ? opts->row_offset : 0;
+    const uint32_t stride = (opts && opts->row_stride > 1) ? opts->row_stride : 1;
+    rtk_frame_desc f_all;
+    if ((rc = init_frame(cam, seed, off, stride, f_all)) != RT_OK) return rc;
+    rt_comm* comm = opts ? opts->comm : nullptr;
+    const uint32_t nd = (opts && opts->n_devices > 1) ? opts->n_devices : 1;
+    if (comm && nd > 1) return set_error(RT_EINVAL, "opts.comm and opts.n_devices > 1 are exclusive");
+    if (nd > 1 && !opts->devices) return set_error(RT_EINVAL, "n_devices > 1 without a device list");
+    if (comm && (comm->rank < 0 || comm->rank >= comm->nranks)) return set_error(RT_EINVAL, "bad communicator");
     const bool reference_bvh = opts && (opts->flags & RT_FLAG_REFERENCE_BVH);
-    if ((rc = prepare(s, world, lights, cam->background_tex, reference_bvh, flatten_ms)) != RT_OK) return rc;
-    DeviceWorld* d = s->dev;
-    if ((rc = ensure_buffers(d, f, dev_out == nullptr)) != RT_OK) return rc;
-    hipError_t e = hipMemsetAsync(d->stats, 0, 2 * sizeof(unsigned long long), stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync stats");
-    f.ev_start = d->ev_start;
-    f.ev_stop = d->ev_stop;
-    d->pending_t0 = std::chrono::steady_clock::now();
-    d->pending_stream = stream;
-    float* out = dev_out ? dev_out : d->out;
-    const bool run = f.rows > 0 && f.max_depth > 0;
-    if (run) {
-        uint8_t* srgb = nullptr;
-        if (want_srgb) {
-            const size_t nb = (size_t)f.W * f.rows * 3;
-            if (nb > d->srgb_bytes) {
-                if (d->srgb) (void)hipFree(d->srgb);
-                d->srgb = nullptr;
-                d->srgb_bytes = 0;
-                if ((e = hipMalloc(&d->srgb, nb)) != hipSuccess) return hip_fail(e, "hipMalloc srgb");
-                d->srgb_bytes = nb;
-            }
-            srgb = d->srgb;
-        }
-        e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, stream, d->tier,
-                             d->grid[d->tier], d->params, d->stack_ovf);
-        if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    } else if (f.rows > 0) {
-        // max_depth == 0: every ray_color returns BLACK (camera.rs:282-284)
-        e = hipMemsetAsync(out, 0, (size_t)f.W * f.rows * 3 * sizeof(float), stream);
-        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync output");
+    hipStream_t user_stream = opts ? (hipStream_t)opts->stream : nullptr;
+
+    int cur = -1;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice (no HIP device)");
+    if (comm && comm->device != cur) return set_error(RT_EINVAL, "communicator belongs to another device");
+    if (!s->rs) s->rs = new RenderState();
+    RenderState* r = s->rs;
+    DeviceGuard guard;
+
+    const uint32_t n_parts = comm ? (uint32_t)comm->nranks : nd;
+    const bool gather = n_parts > 1;
+    const bool is_root = !comm || comm->rank == 0;
+    std::vector<Part> parts(comm ? 1 : nd);
+    for (size_t i = 0; i < parts.size(); ++i) {
+        Part& p = parts[i];
+        const uint32_t k = comm ? (uint32_t)comm->rank : (uint32_t)i;
+        p.slot = i;
+        p.device = comm ? cur : (nd > 1 ? opts->devices[i] : cur);
+        p.row_offset = off + k * stride;
+        p.row_stride = stride * n_parts;
+        p.user_stream = i == 0;
+        p.stream = (i == 0) ? user_stream : nullptr;
+        p.out = gather ? nullptr : dev_out;  // gathered parts render into the slot's buffer
+        p.want_srgb = want_srgb && !gather;  // a gathered frame's bytes come from its f32 values (to_rgb below)
     }
-    d->pending = run;
-    d->pending_samples = (uint64_t)f.W * f.rows * f.S * f.S;
-    d->pending_flatten_ms = flatten_ms;
+    if (r->slots.size() < parts.size()) r->slots.resize(parts.size(), nullptr);
+    FlatWorld fw;
+    r->pending = false;
+    r->t0 = std::chrono::steady_clock::now();
+    if (parts.size() == 1) {
+        run_part(s, r, world, lights, cam, seed, reference_bvh, fw, parts[0]);
+    } else {
+        // one host thread per device: uploads and launches proceed in parallel
+        std::vector<std::thread> th;
+        for (size_t i = 1; i < parts.size(); ++i)
+            th.emplace_back(run_part, s, r, world, lights, cam, seed, reference_bvh, std::ref(fw), std::ref(parts[i]));
+        run_part(s, r, world, lights, cam, seed, reference_bvh, fw, parts[0]);
+        for (auto& t : th) t.join();
+    }
+    double flatten_ms = 0;
+    for (Part& p : parts) {
+        if (p.rc != RT_OK) return set_error(p.rc, p.err);
+        flatten_ms = std::max(flatten_ms, p.flatten_ms);
+    }
+    r->n_parts = (int)parts.size();
+    r->gathered = gather;
+    r->is_root = is_root;
+    r->flatten_ms = flatten_ms;
+    r->root_stream = parts[0].stream;
+    if (gather) {
+        // ---- the framebuffer gather onto the root (one RCCL group)
+        Part& root = parts[0];
+        const uint32_t W = f_all.W, rows = f_all.rows;
+        const size_t slice = (size_t)part_rows(rows, 0, n_parts) * W * 3;  // part 0 has the most rows
+        const size_t row_floats = (size_t)W * 3;
+        RcclApi& nc = rccl();
+        if ((e = hipSetDevice(root.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+        hipStream_t rs = root.stream;
+        if (is_root) {
+            const size_t full = (dev_out ? 0 : rows * row_floats * sizeof(float));
+            const size_t srgb = (host_call && want_srgb) ? rows * row_floats : 0;
+            if ((rc = root_buffers(r, root.device, n_parts * slice * sizeof(float), full, srgb)) != RT_OK) return rc;
+            if ((e = hipEventRecord(r->g_start, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+        }
+        bool distinct = true;
+        for (uint32_t i = 0; i < nd && !comm; ++i)
+            for (uint32_t j = i + 1; j < nd; ++j) distinct = distinct && opts->devices[i] != opts->devices[j];
+        if (comm) {
+            if (!nc.ok) return set_error(RT_EDEVICE, nc.err);
+            ncclResult_t ne = nc.group_start();
+            if (ne == ncclSuccess)
+                ne = nc.send(root.out_used, (size_t)root.rows * row_floats, ncclFloat32, 0, comm->comm, rs);
+            if (ne == ncclSuccess && is_root)
+                for (uint32_t q = 0; q < n_parts && ne == ncclSuccess; ++q)
+                    ne = nc.recv(r->staging + q * slice, (size_t)part_rows(rows, q, n_parts) * row_floats, ncclFloat32,
+                                 (int)q, comm->comm, rs);
+            const ncclResult_t ge = nc.group_end();
+            if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
+            if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+        } else if (distinct && nc.ok) {
+            std::vector<int> devs(opts->devices, opts->devices + nd);
+            if (r->comm_devices != devs) {
+                destroy_comms(r);
+                r->comms.assign(nd, nullptr);
+                ncclResult_t ne = nc.comm_init_all(r->comms.data(), (int)nd, devs.data());
+                if (ne != ncclSuccess) {
+                    r->comms.clear();
+                    return nccl_fail(ne, "ncclCommInitAll");
+                }
+                r->comm_devices = devs;
+            }
+            ncclResult_t ne = nc.group_start();
+            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k)
+                ne = nc.send(parts[k].out_used, (size_t)parts[k].rows * row_floats, ncclFloat32, 0, r->comms[k],
+                             parts[k].stream);
+            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k)
+                ne = nc.recv(r->staging + k * slice, (size_t)parts[k].rows * row_floats, ncclFloat32, (int)k,
+                             r->comms[0], rs);
+            const ncclResult_t ge = nc.group_end();
+            if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
+            if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+        } else {
+            // a device listed twice (one communicator per device is all RCCL
+            // allows) or no librccl: peer copies onto the root
+            for (uint32_t k = 0; k < nd; ++k) {
+                if (!parts[k].rows) continue;
+                if ((e = hipStreamWaitEvent(rs, parts[k].d->ev_done, 0)) != hipSuccess)
+                    return hip_fail(e, "hipStreamWaitEvent");
+                if ((e = hipMemcpyPeerAsync(r->staging + k * slice, root.device, parts[k].out_used, parts[k].device,
+                                            (size_t)parts[k].rows * row_floats * sizeof(float), rs)) != hipSuccess)
+                    return hip_fail(e, "hipMemcpyPeerAsync");
+            }
+        }
+        if (is_root) {
+            float* frame = dev_out ? dev_out : r->full;
+            if ((e = rtk_launch_deinterleave(r->staging, slice, frame, rows, W, n_parts, rs)) != hipSuccess)
+                return hip_fail(e, "deinterleave launch");
+            if (host_call && want_srgb && cam->max_depth > 0 &&
+                (e = rtk_launch_to_rgb(frame, r->full_srgb, (uint64_t)rows * row_floats, cam->toon_map, rs)) != hipSuccess)
+                return hip_fail(e, "to_rgb launch");
+            if (host_call && want_srgb && cam->max_depth == 0 &&
+                (e = hipMemsetAsync(r->full_srgb, 0, (size_t)rows * row_floats, rs)) != hipSuccess)
+                return hip_fail(e, "hipMemsetAsync srgb");
+            if ((e = hipEventRecord(r->g_stop, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+            r->g_recorded = true;
+        }
+        // the root's slot is reused only after the gather read it
+        if ((e = hipEventRecord(root.d->ev_done, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    }
+    r->pending = true;
     return RT_OK;
 }
 
 static int32_t wait(rt_scene* s, rt_stats* st) {
-    DeviceWorld* d = s ? s->dev : nullptr;
+    RenderState* r = s ? s->rs : nullptr;
     if (st) std::memset(st, 0, sizeof(*st));
-    if (!d) return set_error(RT_EINVAL, "nothing rendered on this scene");
-    hipError_t e = hipStreamSynchronize(d->pending_stream);
-    if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
-    unsigned long long h[2] = {0, 0};
-    if ((e = hipMemcpy(h, d->stats, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "stats copy");
-    float ms = 0;
-    if (d->pending) (void)hipEventElapsedTime(&ms, d->ev_start, d->ev_stop);
-    if (st) {
-        st->samples = d->pending_samples;
-        st->rays = h[0];
-        st->panics = h[1];
-        st->kernel_ms = ms;
-        st->flatten_ms = d->pending_flatten_ms;
-        st->render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d->pending_t0).count();
+    if (!r || r->n_parts == 0) return set_error(RT_EINVAL, "nothing rendered on this scene");
+    DeviceGuard guard;
+    uint64_t rays = 0, panics = 0, samples = 0;
+    double kernel_ms = 0;
+    hipError_t e;
+    for (int k = 0; k < r->n_parts; ++k) {
+        DeviceWorld* d = r->slots[k];
+        (void)hipSetDevice(d->device);
+        if ((e = hipStreamSynchronize(d->last_stream)) != hipSuccess) return hip_fail(e, "render (stream synchronize)");
+        unsigned long long h[2] = {0, 0};
+        if ((e = hipMemcpy(h, d->stats, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "stats copy");
+        rays += h[0];
+        panics += h[1];
+        samples += d->samples;
+        float ms = 0;
+        if (d->ran) (void)hipEventElapsedTime(&ms, d->ev_start, d->ev_stop);
+        kernel_ms = std::max(kernel_ms, (double)ms);
     }
-    d->pending = false;
-    if (h[1]) return set_error(RT_EPANIC, std::to_string(h[1]) + " path(s) hit a reference panic condition "
-                                                                "(NaN radiance, zero pdf, non-normalizable vector)");
+    float gms = 0;
+    if (r->gathered && r->is_root) {
+        (void)hipSetDevice(r->root_device);
+        if ((e = hipStreamSynchronize(r->root_stream)) != hipSuccess) return hip_fail(e, "gather (stream synchronize)");
+        (void)hipEventElapsedTime(&gms, r->g_start, r->g_stop);
+    }
+    if (st) {
+        st->samples = samples;
+        st->rays = rays;
+        st->panics = panics;
+        st->n_devices = (uint64_t)r->n_parts;
+        st->kernel_ms = kernel_ms;
+        st->flatten_ms = r->flatten_ms;
+        st->gather_ms = gms;
+        st->render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r->t0).count();
+    }
+    r->pending = false;
+    if (panics) return set_error(RT_EPANIC, std::to_string(panics) + " path(s) hit a reference panic condition "
+                                                                     "(NaN radiance, zero pdf, non-normalizable vector)");
     return RT_OK;
 }
 
@@ -370,9 +794,10 @@ extern "C" {
 
 int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
                          float* out_dev) {
-    if (!out_dev) return set_error(RT_EINVAL, "null device output");
+    const bool root = !(opts && opts->comm) || opts->comm->rank == 0;
+    if (!out_dev && root) return set_error(RT_EINVAL, "null device output");
     try {
-        return launch(s, world, lights, cam, opts, out_dev, opts ? (hipStream_t)opts->stream : nullptr);
+        return launch(s, world, lights, cam, opts, out_dev, false, false);
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }
@@ -411,6 +836,24 @@ int32_t rt_render_device_wait(rt_scene* s, rt_stats* st) {
     return wait(s, st);
 }
 
+int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
+    RenderState* r = s ? s->rs : nullptr;
+    if (!r || r->n_parts != 1 || r->gathered || !r->slots[0])
+        return set_error(RT_EINVAL, "no single-device render on this scene");
+    DeviceWorld* d = r->slots[0];
+    const uint64_t n = (uint64_t)d->W * d->rows * d->S * 3;
+    if (n_values != n) return set_error(RT_EINVAL, "n_values must be rows * W * sqrt_spp * 3 = " + std::to_string(n));
+    if (!d->ran) return set_error(RT_EINVAL, "the last render traced no samples");
+    if (n && !out) return set_error(RT_EINVAL, "null output");
+    DeviceGuard guard;
+    (void)hipSetDevice(d->device);
+    hipError_t e = hipStreamSynchronize(d->last_stream);
+    if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
+    if (n && (e = hipMemcpy(out, d->partial, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy partials");
+    return RT_OK;
+}
+
 int32_t rt_to_rgb_device(const float* lin_dev, uint8_t* srgb_dev, uint64_t n_values, int32_t toon_map, void* stream) {
     if (n_values && (!lin_dev || !srgb_dev)) return set_error(RT_EINVAL, "null argument");
     hipError_t e = rtk_launch_to_rgb(lin_dev, srgb_dev, n_values, toon_map, (hipStream_t)stream);
@@ -419,30 +862,85 @@ int32_t rt_to_rgb_device(const float* lin_dev, uint8_t* srgb_dev, uint64_t n_val
 
 int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
                   float* out_lin, uint8_t* out_srgb, rt_stats* st) {
+    if (!cam) return set_error(RT_EINVAL, "null camera");
     try {
-        hipStream_t stream = opts ? (hipStream_t)opts->stream : nullptr;
         const uint32_t rows = rt_shard_rows(cam, opts);
         const size_t n = (size_t)cam->image_width * rows * 3;
         const bool srgb_dev = out_srgb && cam->max_depth > 0;  // else every pixel is BLACK -> 0
-        int32_t rc = launch(s, world, lights, cam, opts, nullptr, stream, srgb_dev);
+        int32_t rc = launch(s, world, lights, cam, opts, nullptr, true, out_srgb != nullptr);
         if (rc != RT_OK) return rc;
-        DeviceWorld* d = s->dev;
-        hipError_t e = hipStreamSynchronize(stream);
-        if (e != hipSuccess) return hip_fail(e, "render");
-        if (n && out_lin && (e = hipMemcpy(out_lin, d->out, n * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
+        RenderState* r = s->rs;
+        rc = wait(s, st);
+        if (rc != RT_OK && rc != RT_EPANIC) return rc;
+        if (!r->is_root) return rc;
+        DeviceGuard guard;
+        hipError_t e;
+        const float* lin = r->gathered ? r->full : r->slots[0]->out;
+        const uint8_t* sb = r->gathered ? r->full_srgb : r->slots[0]->srgb;
+        (void)hipSetDevice(r->gathered ? r->root_device : r->slots[0]->device);
+        if (n && out_lin && (e = hipMemcpy(out_lin, lin, n * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess)
             return hip_fail(e, "hipMemcpy output");
         if (n && out_srgb) {
-            if (srgb_dev) {
-                if ((e = hipMemcpy(out_srgb, d->srgb, n, hipMemcpyDeviceToHost)) != hipSuccess)
+            if (srgb_dev || r->gathered) {
+                if ((e = hipMemcpy(out_srgb, sb, n, hipMemcpyDeviceToHost)) != hipSuccess)
                     return hip_fail(e, "hipMemcpy srgb");
             } else {
                 std::memset(out_srgb, 0, n);
             }
         }
-        return wait(s, st);
+        return rc;
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }
+}
+
+int32_t rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]) {
+    if (!id) return set_error(RT_EINVAL, "null id");
+    RcclApi& nc = rccl();
+    if (!nc.ok) return set_error(RT_EDEVICE, nc.err);
+    ncclUniqueId u;
+    ncclResult_t e = nc.get_unique_id(&u);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclGetUniqueId");
+    static_assert(sizeof(u) == RT_COMM_ID_BYTES, "ncclUniqueId size");
+    std::memcpy(id, &u, sizeof u);
+    return RT_OK;
+}
+
+rt_comm* rt_comm_init(const uint8_t id[RT_COMM_ID_BYTES], int32_t nranks, int32_t rank) {
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) {
+        set_error(RT_EINVAL, "bad communicator arguments");
+        return nullptr;
+    }
+    RcclApi& nc = rccl();
+    if (!nc.ok) {
+        set_error(RT_EDEVICE, nc.err);
+        return nullptr;
+    }
+    int dev = -1;
+    hipError_t he = hipGetDevice(&dev);
+    if (he != hipSuccess) {
+        hip_fail(he, "hipGetDevice");
+        return nullptr;
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    rt_comm* c = new rt_comm();
+    ncclResult_t e = nc.comm_init_rank(&c->comm, nranks, u, rank);
+    if (e != ncclSuccess) {
+        nccl_fail(e, "ncclCommInitRank");
+        delete c;
+        return nullptr;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = dev;
+    return c;
+}
+
+void rt_comm_destroy(rt_comm* c) {
+    if (!c) return;
+    if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+    delete c;
 }
 
 }  // extern "C"

@@ -1071,7 +1071,7 @@ uint32_t rt_shard_rows(const rt_camera* c, const rt_render_opts* o) {
 
 void rt_scene_destroy(rt_scene* s) {
     if (!s) return;
-    if (s->dev) destroy_device_world(s->dev);
+    if (s->rs) destroy_render_state(s->rs);
     delete s;
 }
 

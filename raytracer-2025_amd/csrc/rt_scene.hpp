@@ -132,7 +132,7 @@ struct HostWorld {
     size_t n_bvh_leaves = 0;
 };
 
-struct DeviceWorld;  // rt_render.hip
+struct RenderState;  // rt_render.cpp: per-device worlds and work buffers
 
 }  // namespace rth
 
@@ -144,8 +144,8 @@ struct rt_scene {
     std::vector<rtk::DPerlin> perlins;
     uint32_t next_medium_id = 0;
     uint64_t generation = 0;  // bumped by every mutation; invalidates the device cache
-    // device-side cache (rt_render.hip)
-    rth::DeviceWorld* dev = nullptr;
+    // device-side cache and the last render's state (rt_render.cpp)
+    rth::RenderState* rs = nullptr;
 };
 
 namespace rth {
@@ -161,5 +161,5 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 // unchanged when it exceeds max_need), or UINT32_MAX (hw unchanged) when the
 // tree would have more than max_nodes nodes.
 uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes = SIZE_MAX);
-void destroy_device_world(DeviceWorld* d);
+void destroy_render_state(RenderState* r);
 }  // namespace rth

@@ -244,11 +244,8 @@ class Camera:
         """pixels x floor(sqrt(spp))^2 -- what camera.rs:183-192 traces."""
         return self.image_width * self.image_height * self.sqrt_spp ** 2
 
-    def render(self, world, lights=None, seed=1, row_offset=0, row_stride=1, threads=0, want_srgb=True, flags=0):
-        """Camera::render (camera.rs:161).  Returns (linear HxWx3 f32, srgb HxWx3 u8 or None, RtStats)."""
-        scene = world.scene
-        api = scene.api
-        cam = self.to_c()
+    @staticmethod
+    def _opts(api, seed, row_offset, row_stride, threads, flags, devices=None, comm=None):
         opts = RtRenderOpts()
         api.render_opts_default(C.byref(opts))
         opts.seed = int(seed)
@@ -256,6 +253,25 @@ class Camera:
         opts.row_stride = int(row_stride)
         opts.threads = int(threads)
         opts.flags = int(flags)
+        keep = None
+        if devices is not None and len(devices) > 1:
+            keep = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+            opts.n_devices = len(devices)
+            opts.devices = C.cast(keep, C.POINTER(C.c_int32))
+        if comm is not None:
+            opts.comm = comm
+        return opts, keep
+
+    def render(self, world, lights=None, seed=1, row_offset=0, row_stride=1, threads=0, want_srgb=True, flags=0,
+               devices=None, comm=None):
+        """Camera::render (camera.rs:161).  Returns (linear HxWx3 f32, srgb HxWx3 u8 or None, RtStats).
+        devices: HIP device ordinals to split the rows over (in-process
+        multi-GPU, one gather onto devices[0]); comm: an rt_comm* of
+        rt_comm_init (one process per GPU; the frame arrives on rank 0)."""
+        scene = world.scene
+        api = scene.api
+        cam = self.to_c()
+        opts, _keep = self._opts(api, seed, row_offset, row_stride, threads, flags, devices, comm)
         rows = api.shard_rows(C.byref(cam), C.byref(opts))
         W = self.image_width
         lin = np.zeros((rows, W, 3), dtype=np.float32)
@@ -266,6 +282,29 @@ class Camera:
                         srgb.ctypes.data_as(C.POINTER(C.c_uint8)) if srgb is not None else None, C.byref(stats))
         api.check(rc)
         return lin, srgb, stats
+
+    def render_partials(self, world, lights=None, seed=1, row_offset=0, row_stride=1, threads=0, flags=0):
+        """Parity tooling: the f64 sum over s_j of ray_color for every (pixel,
+        stratum row s_i) of the shard, (rows, W, sqrt_spp, 3) -- the GPU's
+        per-item sums (rt_render_partials_get) or the oracle's
+        (orc_render_partials).  Returns (partials, RtStats)."""
+        scene = world.scene
+        api = scene.api
+        cam = self.to_c()
+        opts, _keep = self._opts(api, seed, row_offset, row_stride, threads, flags)
+        rows = api.shard_rows(C.byref(cam), C.byref(opts))
+        S = self.sqrt_spp
+        part = np.zeros((rows, self.image_width, S, 3), dtype=np.float64)
+        stats = RtStats()
+        lh = -1 if lights is None else lights.h
+        ptr = part.ctypes.data_as(C.POINTER(C.c_double))
+        if hasattr(api, "render_partials"):  # the oracle
+            api.check(api.render_partials(scene.s, world.h, lh, C.byref(cam), C.byref(opts), ptr, C.byref(stats)))
+        else:
+            api.check(api.render(scene.s, world.h, lh, C.byref(cam), C.byref(opts), None, None, C.byref(stats)))
+            if part.size:
+                api.check(api.render_partials_get(scene.s, ptr, part.size))
+        return part, stats
 
 
 def save_png(api, path, srgb):

@@ -71,3 +71,17 @@ def rmse_per_channel(a, b):
 
     d = a.astype(np.float64) - b.astype(np.float64)
     return np.sqrt((d ** 2).reshape(-1, 3).mean(axis=0))
+
+
+def divergence(g, o, rel=1e-9):
+    """Fraction of (pixel, stratum row) f64 sums whose paths diverged: the GPU
+    runs ray_color as a loop (beta * L) and the oracle as the reference's
+    recursion, so equal paths agree to ~1e-15 relative; a sample that took
+    another branch (a transcendental or contraction ulp flipping a comparison)
+    moves its row sum by orders of magnitude more.  g, o: (..., 3) arrays."""
+    import numpy as np
+
+    g = np.asarray(g, dtype=np.float64).reshape(-1, 3)
+    o = np.asarray(o, dtype=np.float64).reshape(-1, 3)
+    bad = np.any(np.abs(g - o) > rel * np.maximum(1.0, np.abs(o)), axis=1)
+    return float(bad.mean()) if bad.size else 0.0

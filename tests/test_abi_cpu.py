@@ -31,8 +31,9 @@ def test_header_symbols_exported(product, capi):
 def test_oracle_implements_same_abi(oracle, capi):
     # device-side entry points (stream-ordered render, flattened-world info, device to_rgb) have no CPU
     # meaning; PNG / JSON I/O is checked against Python's zlib / json instead (test_output_cpu.py)
+    gpu_only = tuple("orc_" + n for n in capi.GPU_ONLY)
     missing = [m for m in oracle.missing if not m.startswith(("orc_render_device", "orc_world_info", "orc_to_rgb_device",
-                                                             "orc_write_png", "orc_camera_from_json"))]
+                                                             "orc_write_png", "orc_camera_from_json") + gpu_only)]
     assert not missing, missing
 
 
@@ -110,3 +111,22 @@ def test_integration_binds_every_symbol():
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     missing = [s for s in declared_symbols() if "fn " + s + "(" not in text]
     assert not missing, missing
+
+
+def test_null_camera_is_einval(product, rt, scenes):
+    """rt_render / rt_render_device check the camera before touching it or a device."""
+    s = rt.Scene(product)
+    world, lights, cam = scenes.random_spheres(s, 8, 1)
+    assert product.render(s.s, world.h, -1, None, None, None, None, None) == -1
+    assert b"camera" in product.last_error()
+    assert product.render_device(s.s, world.h, -1, None, None, ctypes.c_void_p(16)) == -1
+
+
+def test_comm_and_partials_without_render(product, rt):
+    """Argument checks of the multi-process and parity-tooling entry points
+    (no device needed): bad communicator arguments, partials before a render."""
+    assert not product.comm_init(None, 1, 0)
+    uid = (ctypes.c_uint8 * 128)()
+    assert not product.comm_init(uid, 2, 5)  # rank out of range
+    s = rt.Scene(product)
+    assert product.render_partials_get(s.s, None, 0) == -1

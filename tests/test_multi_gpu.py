@@ -1,0 +1,132 @@
+"""Multi-GPU through the C ABI on the one-GPU box.
+
+The library splits a render into parts -- part k of n renders the shard rows
+k, k + n, ... (camera.rs:178-197's rayon pool, replaced) -- and gathers them
+onto the root: RCCL send/recv in one group between distinct devices (and with
+a communicator from rt_comm_init, one process per GPU), peer copies when a
+device is listed twice.  On one GPU the device list {0, 0} exercises the
+host-thread split, the per-slot device worlds and the re-interleave; a
+one-rank communicator exercises the RCCL group (send to self, receive on the
+root) and the gather events.  Every multi-part frame must equal the
+single-device frame bit for bit (the same (pixel, sample) work, another
+device)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(rt, scenes, api, width=64, spp=4):
+    s = rt.Scene(api)
+    world, lights, cam = scenes.random_spheres(s, width, spp)
+    return s, world, lights, cam
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_device_list_equals_single_device(gpu, rt, scenes, devices):
+    s, world, lights, cam = _scene(rt, scenes, gpu, 70, 9)  # 39 rows: parts of 13 / 13 / 13 and 20 / 19
+    ref, ref_srgb, st0 = cam.render(world, lights, seed=4)
+    lin, srgb, st = cam.render(world, lights, seed=4, devices=devices)
+    np.testing.assert_array_equal(lin, ref)
+    # a gathered frame's bytes are to_rgb of the f32 values (one rounding later than the f64 path)
+    assert np.abs(srgb.astype(int) - ref_srgb.astype(int)).max() <= 1
+    assert st.samples == st0.samples and st.panics == 0
+    assert st.n_devices == max(1, len(devices))
+    if len(devices) > 1:
+        assert st.gather_ms > 0
+    else:
+        assert st.gather_ms == 0
+
+
+def test_device_list_with_shard(gpu, rt, scenes):
+    """A shard (row_offset 1, row_stride 3) split again over two parts."""
+    s, world, lights, cam = _scene(rt, scenes, gpu, 64, 4)
+    ref, _, _ = cam.render(world, lights, seed=2, row_offset=1, row_stride=3, want_srgb=False)
+    lin, _, st = cam.render(world, lights, seed=2, row_offset=1, row_stride=3, want_srgb=False, devices=[0, 0])
+    np.testing.assert_array_equal(lin, ref)
+    assert st.n_devices == 2
+
+
+def test_more_parts_than_rows(gpu, rt, scenes):
+    s, world, lights, cam = _scene(rt, scenes, gpu, 8, 1)  # 4 rows, 5 parts: part 4 renders nothing
+    ref, _, _ = cam.render(world, lights, seed=3, want_srgb=False)
+    lin, _, _ = cam.render(world, lights, seed=3, want_srgb=False, devices=[0, 0, 0, 0, 0])
+    np.testing.assert_array_equal(lin, ref)
+
+
+def test_one_rank_communicator(gpu, rt, scenes, capi):
+    """rt_comm_unique_id / rt_comm_init / an RCCL gather of one rank onto itself."""
+    s, world, lights, cam = _scene(rt, scenes, gpu, 64, 4)
+    ref, _, _ = cam.render(world, lights, seed=5, want_srgb=False)
+    uid = (ctypes.c_uint8 * 128)()
+    gpu.check(gpu.comm_unique_id(uid))
+    comm = gpu.comm_init(uid, 1, 0)
+    assert comm, gpu.last_error()
+    try:
+        lin, _, st = cam.render(world, lights, seed=5, want_srgb=False, comm=comm)
+        np.testing.assert_array_equal(lin, ref)
+        assert st.n_devices == 1 and st.gather_ms > 0
+        lin2, _, _ = cam.render(world, lights, seed=5, want_srgb=False, comm=comm)  # the communicator is reusable
+        np.testing.assert_array_equal(lin2, ref)
+    finally:
+        gpu.comm_destroy(comm)
+
+
+def test_comm_and_devices_are_exclusive(gpu, rt, scenes, capi):
+    s, world, lights, cam = _scene(rt, scenes, gpu, 16, 1)
+    uid = (ctypes.c_uint8 * 128)()
+    gpu.check(gpu.comm_unique_id(uid))
+    comm = gpu.comm_init(uid, 1, 0)
+    try:
+        with pytest.raises(capi.RtError) as e:
+            cam.render(world, lights, comm=comm, devices=[0, 0])
+        assert e.value.code == -1
+    finally:
+        gpu.comm_destroy(comm)
+
+
+def test_render_device_calls_are_ordered(gpu, rt, scenes, capi):
+    """Two rt_render_device calls on one scene, on two streams, without a wait
+    between them: the second's kernels wait for the first's (they share the
+    scene's work buffers), so both frames are right."""
+    import torch
+
+    s, world, lights, cam = _scene(rt, scenes, gpu, 96, 16)
+    ref_a, _, _ = cam.render(world, lights, seed=21, want_srgb=False)
+    ref_b, _, _ = cam.render(world, lights, seed=22, want_srgb=False)
+    c = cam.to_c()
+    outs, streams = [], [torch.cuda.Stream(), torch.cuda.Stream()]
+    for seed, st in zip((21, 22), streams):
+        opts = capi.RtRenderOpts()
+        gpu.render_opts_default(ctypes.byref(opts))
+        opts.seed = seed
+        opts.stream = ctypes.c_void_p(st.cuda_stream)
+        out = torch.empty((cam.image_height, cam.image_width, 3), dtype=torch.float32, device="cuda")
+        gpu.check(gpu.render_device(s.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts),
+                                    ctypes.c_void_p(out.data_ptr())))
+        outs.append(out)
+    stt = capi.RtStats()
+    gpu.check(gpu.render_device_wait(s.s, ctypes.byref(stt)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(outs[0].cpu().numpy(), ref_a)
+    np.testing.assert_array_equal(outs[1].cpu().numpy(), ref_b)
+
+
+def test_render_device_on_device_list(gpu, rt, scenes, capi):
+    """rt_render_device with a device list: the frame lands in the caller's buffer on devices[0]."""
+    import torch
+
+    s, world, lights, cam = _scene(rt, scenes, gpu, 64, 4)
+    ref, _, _ = cam.render(world, lights, seed=8, want_srgb=False)
+    c = cam.to_c()
+    opts, keep = rt.Camera._opts(gpu, 8, 0, 1, 0, 0, devices=[0, 0])
+    out = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.float32, device="cuda")
+    opts.stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    gpu.check(gpu.render_device(s.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts), ctypes.c_void_p(out.data_ptr())))
+    st = capi.RtStats()
+    gpu.check(gpu.render_device_wait(s.s, ctypes.byref(st)))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    assert st.n_devices == 2

@@ -1,22 +1,38 @@
 """GPU parity: librt_mi355x.so (gfx950 kernel, through the C ABI) against the
 TEST-ONLY CPU oracle on the same scene script, camera and RNG seed.
 
-Tolerance (north star): per-channel RMSE < 1e-3 on linear radiance.  The two
+Bar (north star): per-channel RMSE < 1e-3 on linear radiance.  The two
 implementations share the RNG contract (oracle/rng_contract.hpp), so almost
-every sample follows the same path; the residual comes from ulp differences in
-f64 transcendentals and FMA contraction on the GPU, which flip a rare path.
+every sample follows the same path; the measured residual is far below the
+bar, and each test holds it to a tight bound of its own: RMSE, the fraction of
+pixels within 1e-5 relative, and the divergence rate -- the fraction of
+(pixel, stratum row) f64 sums whose paths took another branch (ulp
+differences of f64 transcendentals between ROCm's ocml and glibc flipping a
+comparison).  Every test prints all three.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
-from conftest import rmse_per_channel
+from conftest import divergence, rmse_per_channel
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1e-3
+TOL = 1e-3          # the north-star bar
+RMSE_TIGHT = 1e-5   # what these frames actually hold
 
 
-def render_both(gpu, oracle, rt, build, seed=1, **cam_over):
+def gpu_partials(api, scene, cam, rows):
+    """The f64 (pixel, s_i) sums of the last render on `scene` (rt_render_partials_get)."""
+    part = np.zeros((rows, cam.image_width, cam.sqrt_spp, 3), dtype=np.float64)
+    if part.size:
+        api.check(api.render_partials_get(scene.s, part.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), part.size))
+    return part
+
+
+def render_both(gpu, oracle, rt, build, seed=1, partials=True, **cam_over):
+    """Renders the same scene script on both; out[name] = (linear, srgb, partials or None)."""
     out = {}
     stats = {}
     for name, api in (("gpu", gpu), ("oracle", oracle)):
@@ -25,21 +41,64 @@ def render_both(gpu, oracle, rt, build, seed=1, **cam_over):
         for k, v in cam_over.items():
             setattr(cam, k, v)
         lin, srgb, st = cam.render(world, lights, seed=seed)
-        out[name] = (lin, srgb)
+        part = None
+        if partials and cam.max_depth > 0:
+            if name == "gpu":
+                part = gpu_partials(api, scene, cam, lin.shape[0])
+            else:
+                part, _ = cam.render_partials(world, lights, seed=seed)
+        out[name] = (lin, srgb, part)
         stats[name] = st
     return out, stats
 
 
-def check(out, tol=TOL, min_exact=0.9):
+def check(out, tol=RMSE_TIGHT, min_exact=0.999, max_div=1e-3):
     g, o = out["gpu"][0], out["oracle"][0]
     assert g.shape == o.shape
     assert np.isfinite(g).all()
     rmse = rmse_per_channel(g, o)
     exact = np.mean(np.all(np.abs(g - o) <= 1e-5 * np.maximum(1.0, np.abs(o)), axis=-1))
-    print(f"per-channel RMSE {rmse}, pixels within 1e-5: {exact:.4f}")
+    div = None
+    if out["gpu"][2] is not None:
+        div = divergence(out["gpu"][2], out["oracle"][2])
+    print(f"per-channel RMSE {rmse}, pixels within 1e-5: {exact:.5f}, diverged (pixel, s_i) sums: {div}")
+    assert np.all(rmse < TOL), rmse
     assert np.all(rmse < tol), rmse
     assert exact >= min_exact, exact
+    if div is not None:
+        assert div <= max_div, div
     return rmse
+
+
+def rows_vs_oracle(gpu, oracle, rt, build, seed, shards, full_spp=None):
+    """Full-width shard rows at the config's sample count: GPU rows (and their
+    f64 (pixel, s_i) sums) against the oracle's.  shards: [(row_offset,
+    row_stride)].  With full_spp, the GPU also renders the whole frame at that
+    spp for finiteness and no panics.  Returns (gpu_lin, oracle_lin, gpu_part, oracle_part)."""
+    res = {"gpu": ([], []), "oracle": ([], [])}
+    for name, api in (("gpu", gpu), ("oracle", oracle)):
+        scene = rt.Scene(api)
+        world, lights, cam = build(scene)
+        for off, stride in shards:
+            if name == "gpu":
+                lin, _, st = cam.render(world, lights, seed=seed, row_offset=off, row_stride=stride, want_srgb=False)
+                part = gpu_partials(api, scene, cam, lin.shape[0])
+            else:
+                part, st = cam.render_partials(world, lights, seed=seed, row_offset=off, row_stride=stride)
+                # camera.rs:193: pixel = (sum of the samples) * pixel_sample_scale, to f32 as the GPU's reduce
+                lin = (part.sum(axis=2) * (1.0 / cam.sqrt_spp ** 2)).astype(np.float32)
+            assert st.panics == 0
+            res[name][0].append(lin)
+            res[name][1].append(part)
+        if name == "gpu" and full_spp:
+            spp = cam.samples_per_pixel
+            cam.samples_per_pixel = full_spp
+            full, _, st1 = cam.render(world, lights, seed=seed, want_srgb=False)
+            assert full.shape == (cam.image_height, cam.image_width, 3) and np.isfinite(full).all()
+            assert st1.panics == 0
+            cam.samples_per_pixel = spp
+    cat = lambda xs: np.concatenate(xs, axis=0)
+    return cat(res["gpu"][0]), cat(res["oracle"][0]), cat(res["gpu"][1]), cat(res["oracle"][1])
 
 
 def test_c1_small(gpu, oracle, rt, scenes):
@@ -61,34 +120,56 @@ def test_c2_full_config_rows(gpu, oracle, rt, scenes):
     1920x1080, 512 spp (22^2 = 484 traced), depth 50.  Five shard rows (every
     216th) against the oracle at the full sample count, and the whole frame on
     the GPU for its sample count, finiteness and no panics."""
-    out = {}
-    for name, api in (("gpu", gpu), ("oracle", oracle)):
-        scene = rt.Scene(api)
-        world, lights, cam = scenes.random_spheres(scene, 1920, 512)
+    def build(s):
+        world, lights, cam = scenes.random_spheres(s, 1920, 512)
         assert (cam.image_height, cam.sqrt_spp, cam.max_depth) == (1080, 22, 50)
-        lin, _, st = cam.render(world, lights, seed=1, row_offset=0, row_stride=216)
-        assert lin.shape == (5, 1920, 3) and st.samples == 5 * 1920 * 484 and st.panics == 0
-        out[name] = (lin, None)
-        if name == "gpu":
-            full, _, st1 = cam.render(world, lights, seed=1, want_srgb=False)
-            assert full.shape == (1080, 1920, 3) and np.isfinite(full).all()
-            assert st1.samples == 1920 * 1080 * 484 and st1.panics == 0
-            # rows 0, 216, ... of the whole frame are the shard's rows
-            assert np.array_equal(full[::216], lin)
-    check(out, min_exact=0.99)
+        return world, lights, cam
+    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, build, 1, [(0, 216)], full_spp=512)
+    assert g.shape == (5, 1920, 3)
+    check({"gpu": (g, None, gp), "oracle": (o, None, op)})
+
+
+def test_c3_full_config_rows(gpu, oracle, rt, scenes):
+    """BASELINE configs[2]: the Cornell box + smoke at 800x800, 1024 spp
+    (32^2), depth 10 (main.rs:624) -- rows 0, 400 and 799 at the full sample
+    count against the oracle (quads, Transform, two media, DiffuseLight, the
+    50/50 light-PDF mixture: camera.rs:275-325, volume.rs:37-73,
+    pdf.rs:90-120), and the whole frame at 16 spp on the GPU."""
+    def build(s):
+        world, lights, cam = scenes.cornell_smoke(s, 800, 1024)
+        assert (cam.image_height, cam.sqrt_spp, cam.max_depth) == (800, 32, 10)
+        return world, lights, cam
+    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, build, 1, [(0, 400), (799, 800)], full_spp=16)
+    assert g.shape == (3, 800, 3)
+    check({"gpu": (g, None, gp), "oracle": (o, None, op)})
+
+
+def test_c5_full_config_rows(gpu, oracle, rt, scenes):
+    """BASELINE configs[4] geometry: the book-2 final scene at 3840x2160,
+    depth 40 (main.rs:33), aspect 16/9 -- rows 0, 1080 and 2159 at 256 spp
+    (16^2) against the oracle (moving spheres, Perlin noise, the missing-image
+    cyan, a rotated sphere BVH, two media, the light quad), and the whole
+    frame at 1 spp on the GPU."""
+    def build(s):
+        world, lights, cam = scenes.final_scene(s, 3840, 256, 40, aspect_ratio=16 / 9)
+        assert (cam.image_height, cam.sqrt_spp, cam.max_depth) == (2160, 16, 40)
+        return world, lights, cam
+    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, build, 1, [(0, 1080), (2159, 2160)], full_spp=1)
+    assert g.shape == (3, 3840, 3)
+    check({"gpu": (g, None, gp), "oracle": (o, None, op)})
 
 
 def test_c3_cornell_smoke_small(gpu, oracle, rt, scenes):
     """Quads, Transform, ConstantMedium, Isotropic, DiffuseLight, light-PDF mixture (C3 features)."""
     out, _ = render_both(gpu, oracle, rt, lambda s: scenes.cornell_smoke(s, 96, 16))
-    check(out, min_exact=0.8)
+    check(out)
 
 
 def test_c5_final_scene_small(gpu, oracle, rt, scenes):
     """Moving sphere, noise + missing-image textures, transformed BVH, two media, lights (C5 features)."""
     out, _ = render_both(gpu, oracle, rt,
                          lambda s: scenes.final_scene(s, 128, 16, 40, aspect_ratio=16 / 9))
-    check(out, min_exact=0.7)
+    check(out)
 
 
 def test_shard_rows_equal_full_frame(gpu, rt, scenes):
@@ -321,7 +402,7 @@ def test_c4_obj_full_tier_materials(gpu, oracle, rt, tmp_path):
         return world, None, cam
 
     out, st = render_both(gpu, oracle, rt, build)
-    check(out, min_exact=0.8)
+    check(out)
     assert st["gpu"].panics == st["oracle"].panics
 
 
@@ -330,20 +411,10 @@ def test_c4_full_size_mesh_rows(gpu, oracle, rt, scenes, tmp_path):
     shard rows (0 and 540) at 4 spp against the oracle on the same 1M-triangle
     world, and the whole frame at 1 spp for finiteness / no panics."""
     p = scenes.write_terrain_obj(str(tmp_path), 707)
-    out = {}
-    for name, api in (("gpu", gpu), ("oracle", oracle)):
-        scene = rt.Scene(api)
-        world, lights, cam = scenes.obj_terrain(scene, p, 1920, 4)
-        lin, _, st = cam.render(world, lights, seed=11, row_offset=0, row_stride=540)
-        assert lin.shape == (2, 1920, 3) and st.panics == 0
-        out[name] = lin
-        if name == "gpu":
-            cam.samples_per_pixel = 1
-            full, _, st1 = cam.render(world, lights, seed=11)
-            assert full.shape == (1080, 1920, 3) and np.isfinite(full).all() and st1.panics == 0
-    rmse = rmse_per_channel(out["gpu"], out["oracle"])
-    print("C4 full-size rows RMSE", rmse)
-    assert np.all(rmse < TOL)
+    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, lambda s: scenes.obj_terrain(s, p, 1920, 4), 11, [(0, 540)],
+                                  full_spp=1)
+    assert g.shape == (2, 1920, 3)
+    check({"gpu": (g, None, gp), "oracle": (o, None, op)})
 
 
 def test_c4_obj_missing_normal_map(gpu, oracle, rt, tmp_path):
@@ -372,7 +443,7 @@ def test_c4_obj_missing_normal_map(gpu, oracle, rt, tmp_path):
         return world, None, cam
 
     out, st = render_both(gpu, oracle, rt, build)
-    check(out, min_exact=0.8)
+    check(out)
     assert st["gpu"].panics == st["oracle"].panics
 
 
@@ -429,7 +500,7 @@ def test_sphere_bvh_edge_worlds(gpu, oracle, rt, capi, n, variant):
     import ctypes
     out, st = render_both(gpu, oracle, rt, lambda s: _sphere_bvh_world(s, n, with_quad=variant == "mesh",
                                                                        camera_inside=variant == "inside"))
-    check(out, min_exact=0.97)
+    check(out)
     assert st["gpu"].panics == 0
     s = rt.Scene(gpu)
     w, _, cam = _sphere_bvh_world(s, n, with_quad=variant == "mesh", camera_inside=variant == "inside")
@@ -459,7 +530,7 @@ def test_sphere_worlds_around_the_lds_tree_limit(gpu, oracle, rt, capi, n):
     oracle."""
     import ctypes
     out, st = render_both(gpu, oracle, rt, lambda s: _many_spheres_world(s, n))
-    check(out, min_exact=0.97)
+    check(out)
     assert st["gpu"].panics == 0
     s = rt.Scene(gpu)
     w, _, cam = _many_spheres_world(s, n)
