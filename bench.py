@@ -319,8 +319,8 @@ def main():
         launch_samples = W * launch_rows * sqrt_spp * sqrt_spp
         flops = wc["flops_per_sample"] * launch_samples
         achieved = flops / (kernel_avg_ms * 1e-3) / 1e12
-        traffic, traffic_src = (load_profile_field(f"pmc_{args.workload}.json", "hbm_bytes_per_launch")
-                                if parts == 1 else (None, None))
+        tps, traffic_src = load_profile_field(f"pmc_{args.workload}.json", "hbm_bytes_per_sample")
+        traffic = round(tps * launch_samples) if tps else None
         exec_fps, exec_src = load_profile_field(f"valu_{args.workload}.json", "executed_f64_flops_per_sample")
         n = world_size if distributed else (args.gpus if args.in_process else 1)
         how = ("one frame per step on one GPU" if n == 1 else
@@ -368,7 +368,8 @@ def main():
                               "reference BVH topology (bench_data/work_counts_<workload>.json) per launch / path-kernel "
                               "time (HIP events on the render stream) -- a throughput normalisation, not hardware "
                               "utilisation; frac_executed is the executed-instruction view",
-                "traffic_source": traffic_src,
+                "traffic_source": (traffic_src + " (HBM bytes per traced sample from the rocprofv3 request "
+                                   "counters x this launch's samples)") if traffic_src else None,
             },
         }
         if exec_fps:

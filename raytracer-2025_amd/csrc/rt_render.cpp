@@ -620,7 +620,9 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     DeviceGuard guard;
 
     const uint32_t n_parts = comm ? (uint32_t)comm->nranks : nd;
-    const bool gather = n_parts > 1;
+    // with a communicator the frame always goes through the RCCL group (a
+    // one-rank communicator sends to itself), so every rank count runs one path
+    const bool gather = n_parts > 1 || comm;
     const bool is_root = !comm || comm->rank == 0;
     std::vector<Part> parts(comm ? 1 : nd);
     for (size_t i = 0; i < parts.size(); ++i) {

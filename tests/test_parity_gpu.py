@@ -156,7 +156,10 @@ def test_c5_full_config_rows(gpu, oracle, rt, scenes):
         return world, lights, cam
     g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, build, 1, [(0, 1080), (2159, 2160)], full_spp=1)
     assert g.shape == (3, 3840, 3)
-    check({"gpu": (g, None, gp), "oracle": (o, None, op)})
+    # measured: 1.1e-3 of the (pixel, s_i) sums diverge (ocml vs glibc f64
+    # transcendentals over 40-bounce paths in media; 1.1e-3 with contraction
+    # off too), RMSE 5e-8
+    check({"gpu": (g, None, gp), "oracle": (o, None, op)}, max_div=3e-3, tol=1e-6)
 
 
 def test_c3_cornell_smoke_small(gpu, oracle, rt, scenes):
