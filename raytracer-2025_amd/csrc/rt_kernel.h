@@ -43,12 +43,17 @@ namespace rtk {
 //         and textures: C3, C5).
 //  FULL_FLAT: FULL for worlds without any BVH node (C3): the walk carries no
 //         BVH code, which leaves the registers to the rest (fewer spills).
-enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2, TIER_FULL_FLAT = 3 };
-constexpr int N_TIERS = 4;
+//  FULL_GL: FULL with general lights (Transforms, nested lists, moving
+//         spheres in the lights tree); kept apart so that the light-tree
+//         code does not weigh on the C3 / C5 tiers.
+enum Tier : int { TIER_BASIC = 0, TIER_MESH = 1, TIER_FULL = 2, TIER_FULL_FLAT = 3, TIER_FULL_GL = 4 };
+constexpr int N_TIERS = 5;
 __host__ __device__ constexpr bool tier_full(int t) { return t >= TIER_FULL; }
+// full tiers that walk BVH nodes
+__host__ __device__ constexpr bool tier_full_bvh(int t) { return t == TIER_FULL || t == TIER_FULL_GL; }
 // traversal-stack entries a lane keeps in LDS (deeper ones: global overflow column)
 __host__ __device__ constexpr uint32_t lds_stack_entries(int t) {
-    return t == TIER_BASIC ? RT_STACK_BASIC : t == TIER_MESH ? RT_STACK_MESH : t == TIER_FULL ? RT_STACK_FULL : RT_STACK_FLAT;
+    return t == TIER_BASIC ? RT_STACK_BASIC : t == TIER_MESH ? RT_STACK_MESH : tier_full_bvh(t) ? RT_STACK_FULL : RT_STACK_FLAT;
 }
 }  // namespace rtk
 

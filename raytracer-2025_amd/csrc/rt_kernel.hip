@@ -632,7 +632,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
     if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
-        if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (TIER == TIER_FULL && RT_FULL_BVH4))
+        if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4))
             T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
         else
             T.cur = visit_node(S, idx, r, T.rf, T.a, T.inva, tmin, tmin_f, T.cl, stk, T.sp, record);
@@ -1056,15 +1056,9 @@ __device__ __forceinline__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21,
     const D3 w = cross(u, n);
     return v.x * u + v.y * n + v.z * w;
 }
-__device__ D3 light_random(const SceneView& S, D3 o, Rng& rng, uint32_t& ovf, bool& ok) {
-    uint32_t ref = S.lights_root;
-    if (ref_kind(ref) == K_LIST) {  // hits.rs:69-75 choose
-        uint32_t n = 0;
-        for (uint32_t i = ref_index(ref); S.list_children[i] != REF_NONE; ++i) ++n;
-        uint32_t k = (uint32_t)(rng.next(ovf) * (double)n);
-        if (k >= n) k = n - 1;
-        ref = S.list_children[ref_index(ref) + k];
-    }
+// Quad / Triangle / Sphere::random (quad.rs:122-125, triangle.rs:117-128, sphere.rs:134-144)
+__device__ __forceinline__ D3 light_random_one(const SceneView& S, uint32_t ref, D3 o, Rng& rng, uint32_t& ovf,
+                                               bool& ok) {
     const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
     if (kind == K_QUAD || kind == K_TRI) {  // quad.rs:122-125, triangle.rs:117-128
         const DPlanar& P = S.planars[idx];
@@ -1093,6 +1087,102 @@ __device__ D3 light_random(const SceneView& S, D3 o, Rng& rng, uint32_t& ovf, bo
     const D3 res = unit(wv, ok3);
     ok = ok1 && ok2 && ok3;
     return res;
+}
+__device__ D3 light_random(const SceneView& S, D3 o, Rng& rng, uint32_t& ovf, bool& ok) {
+    uint32_t ref = S.lights_root;
+    if (ref_kind(ref) == K_LIST) {  // hits.rs:69-75 choose
+        uint32_t n = 0;
+        for (uint32_t i = ref_index(ref); S.list_children[i] != REF_NONE; ++i) ++n;
+        uint32_t k = (uint32_t)(rng.next(ovf) * (double)n);
+        if (k >= n) k = n - 1;
+        ref = S.list_children[ref_index(ref) + k];
+    }
+    return light_random_one(S, ref, o, rng, ovf, ok);
+}
+
+// ---- general lights (tier FULL_GL): any tree of Hittables lists and
+// Transforms over spheres (static or moving: pdf_value / random use the
+// center at time 0, sphere.rs:114-144), quads and triangles.
+// Hittables::pdf_value averages its children's values in order
+// (hits.rs:52-67); Hittables::random draws one child (hits.rs:69-75);
+// Transform maps the origin and direction into its frame and the sampled
+// point back out (shapes.rs:117-132).  The tree is walked by compile-time
+// recursion over its depth (the flattener rejects deeper trees), as a
+// reference call chain would.
+constexpr int RT_LIGHT_DEPTH = 4;  // list / Transform levels of a lights tree (rt_scene.cpp light_tree_ok)
+
+__device__ double light_pdf_leaf(const SceneView& S, uint32_t ref, D3 o, D3 d) {
+    if (ref_kind(ref) != K_MSPHERE) return light_pdf_one(S, ref, o, d);
+    const double4 s = S.msph_center[ref_index(ref)];  // Ray::new: time 0 (ray.rs:11-17) -> center.at(0)
+    const Ray r{o, d, 0.0};
+    double t;
+    if (!sphere_t(d3(s.x, s.y, s.z), s.w, r, len2(d), 1e-8, __builtin_huge_val(), t)) return 0.0;
+    const double dist_squared = len2(d3(s.x, s.y, s.z) - o);
+    const double ctm = sqrt(1.0 - s.w * s.w / dist_squared);
+    if (isnan(ctm)) return 1.0 / (4.0 * PI);
+    return 1.0 / (2.0 * PI * (1.0 - ctm));
+}
+
+template <int D>
+__device__ double light_pdf_tree(const SceneView& S, uint32_t ref, D3 o, D3 d, bool& panic) {
+    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    if constexpr (D > 0) {
+        if (kind == K_LIST) {  // hits.rs:52-67
+            double sum = 0.0;
+            uint32_t n = 0;
+            for (uint32_t i = idx; S.list_children[i] != REF_NONE; ++i, ++n)
+                sum += light_pdf_tree<D - 1>(S, S.list_children[i], o, d, panic);
+            const double ret = sum / (double)n;
+            if (isnan(ret)) panic = true;  // "The sum of pdf is NaN!"
+            return ret;
+        }
+        if (kind == K_XFORM) {  // shapes.rs:117-123
+            const DXform& X = S.xforms[idx];
+            const D3 lo = xf_in(X, o);
+            const D3 lt = xf_in(X, o + d);
+            return light_pdf_tree<D - 1>(S, X.child, lo, lt - lo, panic);
+        }
+    }
+    return light_pdf_leaf(S, ref, o, d);
+}
+
+template <int D>
+__device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng, uint32_t& ovf, bool& ok) {
+    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    if constexpr (D > 0) {
+        if (kind == K_LIST) {  // hits.rs:69-75 choose
+            uint32_t n = 0;
+            for (uint32_t i = idx; S.list_children[i] != REF_NONE; ++i) ++n;
+            uint32_t k = (uint32_t)(rng.next(ovf) * (double)n);
+            if (k >= n) k = n - 1;
+            return light_random_tree<D - 1>(S, S.list_children[idx + k], o, rng, ovf, ok);
+        }
+        if (kind == K_XFORM) {  // shapes.rs:125-132
+            const DXform& X = S.xforms[idx];
+            const D3 lo = xf_in(X, o);
+            const D3 ld = light_random_tree<D - 1>(S, X.child, lo, rng, ovf, ok);
+            const D3 world_to = xf_out(X, lo + ld);
+            bool ok2;
+            const D3 res = unit(world_to - o, ok2);  // "Random direction can't be normalized!"
+            ok = ok && ok2;
+            return res;
+        }
+    }
+    if (kind == K_MSPHERE) {  // sphere.rs:134-144 with center.at(0)
+        const double4 s = S.msph_center[idx];
+        const D3 direction = d3(s.x, s.y, s.z) - o;
+        const double distance_squared = len2(direction);
+        bool ok1, ok2, ok3;
+        const D3 nd = unit(direction, ok1);
+        const double r1 = rng.next(ovf), r2 = rng.next(ovf);
+        const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
+        const double phi = 2.0 * PI * r1;
+        const double x = cos(phi) * sqrt(1.0 - y * y), z = sin(phi) * sqrt(1.0 - y * y);
+        const D3 res = unit(onb_world(nd, d3(x, y, z), ok2), ok3);
+        ok = ok1 && ok2 && ok3;
+        return res;
+    }
+    return light_random_one(S, ref, o, rng, ovf, ok);
 }
 
 // vec3.rs:313-322
@@ -1264,7 +1354,10 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 dir = random_unit_vector(rng, ovf);
             }
         } else {
-            dir = light_random(S, rec.p, rng, ovf, ok);
+            if constexpr (TIER == TIER_FULL_GL)
+                dir = light_random_tree<RT_LIGHT_DEPTH>(S, S.lights_root, rec.p, rng, ovf, ok);
+            else
+                dir = light_random(S, rec.p, rng, ovf, ok);
         }
         if (!ok) panic = true;
         // value (pdf.rs:22-28, 50-57, 101-111)
@@ -1283,7 +1376,11 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             f = divs(albedo, 4.0 * PI);
         }
         if (use_lights) {
-            const double pdf1 = light_pdf(S, rec.p, dir);
+            double pdf1;
+            if constexpr (TIER == TIER_FULL_GL)
+                pdf1 = light_pdf_tree<RT_LIGHT_DEPTH>(S, S.lights_root, rec.p, dir, panic);
+            else
+                pdf1 = light_pdf(S, rec.p, dir);
             if (isnan(pdf1)) panic = true;
             if (pdf == 0.0 && pdf1 == 0.0) panic = true;
             pdf = pdf * 0.5 + pdf1 * 0.5;
@@ -1348,7 +1445,7 @@ struct KParams {
 };
 
 template <int TIER>
-__global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : TIER == TIER_FULL ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
+__global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : tier_full_bvh(TIER) ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
@@ -1603,6 +1700,9 @@ RT_TIER_ENTRY(2)
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 3
 RT_TIER_ENTRY(3)
 #endif
+#if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 4
+RT_TIER_ENTRY(4)
+#endif
 #if defined(RT_DIAG)
 // diagnostic build: the counters live with the (DIAG_TIER) kernel that adds to them
 extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
@@ -1621,10 +1721,12 @@ extern "C" hipError_t rtk_launch_path_0(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_1(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_2(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_3(int, hipStream_t, const rtk::KParams*);
+extern "C" hipError_t rtk_launch_path_4(int, hipStream_t, const rtk::KParams*);
 extern "C" int rtk_occupancy_0(int*);
 extern "C" int rtk_occupancy_1(int*);
 extern "C" int rtk_occupancy_2(int*);
 extern "C" int rtk_occupancy_3(int*);
+extern "C" int rtk_occupancy_4(int*);
 
 namespace rtk {
 // Color::to_rgb (utils/color.rs:14-36): optional ACES fit, clamp, then the sRGB
@@ -1690,6 +1792,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const float* __res
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL |
                           rtk::F_NORMALMAP;
+    if (features & rtk::F_GENLIGHTS) return rtk::TIER_FULL_GL;
     if (features & full) return rtk::TIER_FULL;
     if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;
@@ -1742,7 +1845,8 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     e = tier == rtk::TIER_BASIC  ? rtk_launch_path_0(grid, stream, Pd)
         : tier == rtk::TIER_MESH ? rtk_launch_path_1(grid, stream, Pd)
         : tier == rtk::TIER_FULL ? rtk_launch_path_2(grid, stream, Pd)
-                                 : rtk_launch_path_3(grid, stream, Pd);
+        : tier == rtk::TIER_FULL_FLAT ? rtk_launch_path_3(grid, stream, Pd)
+                                      : rtk_launch_path_4(grid, stream, Pd);
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
@@ -1773,6 +1877,7 @@ extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {
     return tier == rtk::TIER_BASIC  ? rtk_occupancy_0(blocks_per_cu)
          : tier == rtk::TIER_MESH ? rtk_occupancy_1(blocks_per_cu)
          : tier == rtk::TIER_FULL ? rtk_occupancy_2(blocks_per_cu)
-                                  : rtk_occupancy_3(blocks_per_cu);
+         : tier == rtk::TIER_FULL_FLAT ? rtk_occupancy_3(blocks_per_cu)
+                                       : rtk_occupancy_4(blocks_per_cu);
 }
 #endif  // !RT_TIER_ONLY

@@ -218,7 +218,7 @@ static int prepare_tier(HostWorld& hw) {
     if (tier == rtk::TIER_MESH && rtk_mesh_bvh4() && bvh4_convert(hw, RT_STACK_MAX, false) > RT_STACK_MAX)
         tier = rtk::TIER_FULL;
     if (tier == rtk::TIER_FULL && hw.nodes.empty()) return rtk::TIER_FULL_FLAT;
-    if (tier == rtk::TIER_FULL && rtk_full_bvh4()) {
+    if (rtk::tier_full_bvh(tier) && rtk_full_bvh4()) {
         const uint32_t need = bvh4_convert(hw, RT_STACK_MAX, false);
         if (need > RT_STACK_MAX) {
             set_error(RT_ESTACK, "world needs " + std::to_string(need) + " traversal-stack entries, kernel has " +

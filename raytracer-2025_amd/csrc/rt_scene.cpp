@@ -509,19 +509,55 @@ struct Flattener {
     }
 };
 
-bool light_ok(const rt_scene* s, int id, int depth) {
+// The lights tree of HittablePDF (camera.rs:298-304): 1 = a primitive or one
+// flat list of static spheres / quads / triangles (the FULL tiers' light
+// code), 2 = any other tree of lists and Transforms over spheres (static or
+// moving), quads and triangles (tier FULL_GL: hits.rs:52-75, shapes.rs:117-132),
+// or an RT_E* code: a BVH or a ConstantMedium has no pdf_value / random
+// (hit.rs:52-60 unimplemented!(): the reference panics at the first light
+// sample), an empty list panics in Hittables::random (hits.rs:71-73).
+constexpr int LIGHT_TREE_DEPTH = 4;  // rt_kernel.hip RT_LIGHT_DEPTH
+int light_tree(const rt_scene* s, int id, int depth, std::string& err) {
     const Obj& o = s->objs[id];
     switch (o.kind) {
         case O_SPHERE:
         case O_QUAD:
-        case O_TRI: return true;
-        case O_LIST:
-            if (depth > 0 || o.children.empty()) return false;
-            for (int c : o.children)
-                if (!light_ok(s, c, depth + 1)) return false;
-            return true;
-        default: return false;
+        case O_TRI: return 1;
+        case O_MSPHERE: return 2;
+        case O_LIST: {
+            if (o.children.empty()) {
+                err = "The collection of objects is empty! (Hittables::random of the lights, hits.rs:71-73)";
+                return RT_EPANIC;
+            }
+            if (depth >= LIGHT_TREE_DEPTH) {
+                err = "lights tree deeper than " + std::to_string(LIGHT_TREE_DEPTH) + " list / Transform levels";
+                return RT_EUNSUPPORTED;
+            }
+            int kind = depth == 0 ? 1 : 2;
+            for (int c : o.children) {
+                const ObjKind ck = s->objs[c].kind;
+                int k = light_tree(s, c, depth + 1, err);
+                if (k < 0) return k;
+                if (k == 2 || !(ck == O_SPHERE || ck == O_QUAD || ck == O_TRI)) kind = 2;
+            }
+            return kind;
+        }
+        case O_XFORM: {
+            if (depth >= LIGHT_TREE_DEPTH) {
+                err = "lights tree deeper than " + std::to_string(LIGHT_TREE_DEPTH) + " list / Transform levels";
+                return RT_EUNSUPPORTED;
+            }
+            int k = light_tree(s, o.child, depth + 1, err);
+            return k < 0 ? k : 2;
+        }
+        case O_BVH:
+            err = "pdf_value: unimplemented!() -- BVH has no Hittable::pdf_value / random (bvh.rs, hit.rs:52-60)";
+            return RT_EPANIC;
+        case O_MEDIUM:
+            err = "pdf_value: unimplemented!() -- ConstantMedium has no Hittable::pdf_value / random (volume.rs, hit.rs:52-60)";
+            return RT_EPANIC;
     }
+    return RT_EUNSUPPORTED;
 }
 }  // namespace
 
@@ -591,9 +627,10 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
     out.stack_need = 1 + W.second;
     out.lights_root = rtk::REF_NONE;
     if (lights >= 0) {
-        if (!light_ok(s, lights, 0))
-            return set_error(RT_EUNSUPPORTED,
-                             "lights must be a Sphere/Quad/Triangle or a non-empty Hittables of them on the kernel path");
+        std::string lerr;
+        const int lk = light_tree(s, lights, 0, lerr);
+        if (lk < 0) return set_error(lk, lerr);
+        if (lk == 2) out.features |= rtk::F_GENLIGHTS;
         F.no_collapse = true;
         F.memo.erase(lights);
         auto Lr = F.emit(lights, false, 0);

@@ -267,7 +267,7 @@ def test_errors_are_loud(gpu, rt, scenes, capi):
     bvh_lights = scene.BVH(scene.Hittables() if False else _list_of_one(scene))
     with pytest.raises(capi.RtError) as e:
         cam.render(world, bvh_lights)
-    assert e.value.code == -6  # RT_EUNSUPPORTED: lights must be primitives / a list of them
+    assert e.value.code == -5  # RT_EPANIC: BVH has no pdf_value (hit.rs:52-60 unimplemented!())
 
 
 def _list_of_one(scene):
