@@ -240,17 +240,29 @@ def main():
     c = cam.to_c()
     lib_gather = distributed and args.backend == "nccl"
     comm = None
+    gather_note = None
     if lib_gather:
         # the frame gather is the library's RCCL group; the id travels over the torch process group
         uid = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            api.check(api.comm_unique_id(uid))
-        box = [bytes(uid)]
+        ok = 1
+        if rank == 0 and api.comm_unique_id(uid) != 0:
+            ok = 0
+        box = [bytes(uid), ok]
         dist.broadcast_object_list(box, src=0)
         uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
-        comm = api.comm_init(uid, world_size, rank)
-        if not comm:
-            raise RuntimeError("rt_comm_init: " + api.last_error().decode())
+        comm = api.comm_init(uid, world_size, rank) if box[1] else None
+        # every rank must agree on the path: fall back to the torch gather
+        # (harness) only if some rank could not build the communicator
+        flag = torch.tensor([1 if comm else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if flag.item() == 0:
+            gather_note = "rt_comm_init failed (" + (api.last_error() or b"").decode() + "): torch gather instead"
+            if comm:
+                api.comm_destroy(comm)
+            comm = None
+            lib_gather = False
+            print("bench.py: " + gather_note, file=sys.stderr, flush=True)
+    if lib_gather:
         opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0, comm=comm)
         rows = H if rank == 0 else 0
     elif args.in_process:
@@ -282,7 +294,8 @@ def main():
         if rank == 0 and st.kernel_ms > 5000.0:  # long frames (C5 on few GPUs): show progress
             print("bench.py: frame %.1f s" % (st.kernel_ms / 1e3), file=sys.stderr, flush=True)
         if distributed and not lib_gather:
-            frame = pdist.gather_frame(out[:rows].cpu(), H, W)
+            shard = out[:rows] if args.backend == "nccl" else out[:rows].cpu()
+            frame = pdist.gather_frame(shard, H, W)
         else:
             frame = out
         return frame, st
@@ -327,7 +340,7 @@ def main():
                f"one frame per step, rows interleaved over {n} GPUs, " +
                ("RCCL gather to rank 0 inside librt_mi355x.so (rt_comm_init)" if lib_gather else
                 "RCCL gather onto device 0 inside librt_mi355x.so (rt_render_opts.devices)" if args.in_process else
-                "torch gather to rank 0 (gloo rehearsal harness)"))
+                "torch gather to rank 0 (" + (gather_note or "gloo rehearsal harness") + ")"))
         line = {
             "metric": {"c2": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
                        "c3": "Msamples/s (pixels x traced spp / s), book-2 Cornell box + smoke 800x800, 1024 spp",

@@ -24,7 +24,7 @@
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
 #ifndef RT_STACK_FLAT
-#define RT_STACK_FLAT 8     // full-flat tier (lists only: C3 needs few entries); deeper ones overflow
+#define RT_STACK_FLAT 4     // full-flat tier (lists only: C3 needs 4); deeper ones overflow
 #endif
 #ifndef RT_FLAT_LDS_STATE
 #define RT_FLAT_LDS_STATE 1 // full-flat tier: beta, L, acc and the item fields live in LDS across the walk

@@ -49,7 +49,7 @@ namespace rtk {
 // compiles all of it away.
 struct Diag {
 #ifdef RT_DIAG
-    unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0;
+    unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0, cyc_media = 0;
     unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
     unsigned long long load_cyc = 0, loads = 0;  // -DRT_DIAG_LOADLAT: node-load latency (first active lane)
     unsigned long long pops = 0, pop_reads = 0;  // basic tier: pops and the stack entries they read
@@ -395,6 +395,46 @@ __device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t
 }
 
 constexpr float NO_CULL = -__builtin_huge_valf();
+#ifndef RT_FLAT_LIST_BOXES
+#define RT_FLAT_LIST_BOXES 0  // 1: the flat tier tests list elements' f32 boxes first (C3 -4.6 %: not kept)
+#endif
+template <int TIER>
+constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXES; }
+#ifndef RT_FLAT_BOUNDARY_BOXES
+#define RT_FLAT_BOUNDARY_BOXES 0  // the medium boundary walks test element boxes too
+#endif
+
+// The flat tier's list step tests an element's f32 box (list_boxes, rounded
+// outward; the conservative slab of rt_slab.h) before the element: a ray
+// that misses the box within [tmin, c] cannot hit the element closer than c
+// (for a ConstantMedium: cannot enter its boundary there), so skipping it
+// keeps the list's closest hit -- the role a BVH node's boxes play, without
+// the BVH code.
+// Flat tier: the f32 ray of the walk lives in LDS ([3][block] float4 per
+// lane), read by the element box tests only -- 12 registers the walk's
+// other state needs more (152 B/lane of spills with it in registers).
+__device__ __forceinline__ void store_rayf(float4* p, const RayF& R) {
+    p[0] = make_float4(R.idl[0], R.idl[1], R.idl[2], R.idh[0]);
+    p[RT_BLOCK] = make_float4(R.idh[1], R.idh[2], R.nlo[0], R.nlo[1]);
+    p[2 * RT_BLOCK] = make_float4(R.nlo[2], R.nhi[0], R.nhi[1], R.nhi[2]);
+}
+__device__ __forceinline__ RayF load_rayf(const float4* p) {
+    const float4 a = p[0], b = p[RT_BLOCK], c = p[2 * RT_BLOCK];
+    RayF R;
+    R.idl[0] = a.x, R.idl[1] = a.y, R.idl[2] = a.z, R.idh[0] = a.w;
+    R.idh[1] = b.x, R.idh[2] = b.y, R.nlo[0] = b.z, R.nlo[1] = b.w;
+    R.nlo[2] = c.x, R.nhi[0] = c.y, R.nhi[1] = c.z, R.nhi[2] = c.w;
+    return R;
+}
+
+__device__ __forceinline__ bool list_box_hit(const SceneView& S, uint32_t li, const RayF& rf, float tmin_f,
+                                             float c_f) {
+    const RT_GLOBAL float4* bp = reinterpret_cast<const RT_GLOBAL float4*>(S.list_boxes + li);
+    const float4 b0 = bp[0], b1 = bp[1];
+    const float lo[3] = {b0.x, b0.y, b0.z}, hi[3] = {b0.w, b1.x, b1.y};
+    float e;
+    return slab_f(lo, hi, rf, tmin_f, c_f, e);
+}
 
 // Closest t of a medium boundary (no media inside, no records) -- the two
 // boundary.hit calls of volume.rs:44-48.
@@ -425,6 +465,12 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             cur = REF_NONE;
             if (child == REF_NONE) continue;
             const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
+            if constexpr (!BVH && RT_FLAT_BOUNDARY_BOXES && RT_FLAT_LIST_BOXES) {
+                if (!list_box_hit(S, li, rf, tmin_f, cl.c_f)) {
+                    cur = nxt;
+                    continue;
+                }
+            }
             const uint32_t ck = ref_kind(child);
             if (ck == K_SPHERE || ck == K_QUAD || ck == K_TRI || ck == K_MSPHERE) {
                 cur = child;
@@ -555,9 +601,12 @@ struct Trav {
 };
 
 template <int TIER>
-__device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, Trav<TIER>& T) {
+__device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, Trav<TIER>& T, float4* rfl) {
     T.r = wr;
-    T.rf = make_rayf(wr);
+    if constexpr (flat_boxes<TIER>())
+        store_rayf(rfl, make_rayf(wr));
+    else
+        T.rf = make_rayf(wr);
     T.a = len2(wr.d);
     T.inva = 1.0 / T.a;
     T.cl.c = __builtin_huge_val();
@@ -578,7 +627,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
 template <int TIER>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                           const Rng& rng, uint4* med, Diag& dg) {
+                                           const Rng& rng, uint4* med, float4* rfl, Diag& dg) {
     constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
@@ -607,6 +656,12 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         const uint32_t child = S.list_children[li];
         if (child == REF_NONE) return true;  // empty list
         const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
+        if constexpr (flat_boxes<TIER>()) {
+            if (!list_box_hit(S, li, load_rayf(rfl), tmin_f, T.cl.c_f)) {
+                T.cur = nxt;
+                return true;
+            }
+        }
         const uint32_t ck = ref_kind(child);
         if (ck == K_SPHERE || ck == K_QUAD || ck == K_TRI || (FULL && ck == K_MSPHERE)) {
             cur = child;
@@ -656,7 +711,10 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 stk.push(T.sp++, make_ref(K_POPXF, 0), NO_CULL);
                 T.xfs.set(T.nxf++, idx);
                 T.r = xf_ray(X, T.r);
-                T.rf = make_rayf(T.r);
+                if constexpr (flat_boxes<TIER>())
+                    store_rayf(rfl, make_rayf(T.r));
+                else
+                    T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
                 T.inva = 1.0 / T.a;
                 T.cur = X.child;
@@ -666,7 +724,10 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 --T.nxf;
                 T.r = wr;
                 for (uint32_t k = 0; k < T.nxf; ++k) T.r = xf_ray(S.xforms[T.xfs.get(k)], T.r);
-                T.rf = make_rayf(T.r);
+                if constexpr (flat_boxes<TIER>())
+                    store_rayf(rfl, make_rayf(T.r));
+                else
+                    T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
                 T.inva = 1.0 / T.a;
                 break;
@@ -1478,6 +1539,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     __shared__ uint4 pitem_lds[LDS_STATE ? RT_BLOCK : 1];
     double* pst = pstate_lds + threadIdx.x;
     uint4* pit = pitem_lds + threadIdx.x;
+    __shared__ float4 rayf_lds[flat_boxes<TIER>() ? 3 * RT_BLOCK : 1];
+    float4* rfl = rayf_lds + threadIdx.x;
 
     Rng rng;
     rng.k0 = F.key0;
@@ -1577,7 +1640,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         if (!walking) {
             rng.begin(vertex);
             ++n_rays;
-            trace_begin<TIER>(S, ray, T);
+            trace_begin<TIER>(S, ray, T, rfl);
             walking = true;
         }
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
@@ -1589,7 +1652,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 return trace4_step(S, ray, T, stk, pq, node_lds, dg);
             } else {
                 RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
-                return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                return trace_step<TIER>(S, ray, T, stk, rng, med, rfl, dg);
             }
         };
         if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
@@ -1600,7 +1663,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 *pit = make_uint4(item, s_j, px, py);
             }
             while (walking) walking = step();
+            RT_DIAG_ONLY(const unsigned long long t_m0 = __builtin_amdgcn_s_memtime();)
             if constexpr (tier_full(TIER)) media_phase<TIER>(S, ray, T, stk, rng, med);
+            RT_DIAG_ONLY(dg.cyc_media += __builtin_amdgcn_s_memtime() - t_m0;)
             if constexpr (LDS_STATE) {
                 beta = d3(pst[0 * RT_BLOCK], pst[1 * RT_BLOCK], pst[2 * RT_BLOCK]);
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
@@ -1656,6 +1721,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         atomicAdd(&g_diag[1], dg.cyc_trace);
         atomicAdd(&g_diag[2], dg.cyc_shade);
         atomicAdd(&g_diag[4], dg.main_iters);
+        atomicAdd(&g_diag[13], dg.cyc_media);
     }
     atomicAdd(&g_diag[3], dg.wave_trace_iters);  // counted by the first active lane of each wave iteration
     atomicAdd(&g_diag[5], dg.lane_trace_iters);

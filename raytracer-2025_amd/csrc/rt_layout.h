@@ -86,6 +86,14 @@ struct alignas(16) DNode4 {
 };
 static_assert(sizeof(DNode4) == 112, "DNode4 must be 112 B (7 dwordx4)");
 
+// f32 box of one list element (list_boxes, parallel to list_children),
+// rounded outward: the flat tier tests it before the element itself.
+struct alignas(16) DBoxF {
+    float lo[3], hi[3];
+    uint32_t pad[2];
+};
+static_assert(sizeof(DBoxF) == 32, "DBoxF must be 32 B (2 dwordx4)");
+
 // Planar: quad.rs:17-27 / triangle.rs:16-26 hot fields, packed in 128 B:
 // f[0..3) unit normal, f[3] parm_d, f[4..7) anchor, f[7..10) u, f[10..13) v,
 // f[13..16) w = n / |n|^2.
@@ -192,6 +200,7 @@ struct SceneView {
     const RT_GLOBAL DRemap* remaps;
     const RT_GLOBAL DRemapNM* remap_nm;
     const RT_GLOBAL uint32_t* list_children;  // runs of refs, each run terminated by REF_NONE
+    const RT_GLOBAL DBoxF* list_boxes;        // the f32 box of each list_children entry (flat tier)
     const RT_GLOBAL DXform* xforms;
     const RT_GLOBAL DMedium* media;
     const RT_GLOBAL DMaterial* materials;

@@ -297,6 +297,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.remap_nm = (const rtk::DRemapNM*)off(
         put(blob, (hw.features & rtk::F_NORMALMAP) ? hw.remap_nm : std::vector<rtk::DRemapNM>()));
     v.list_children = (const uint32_t*)off(put(blob, hw.list_children));
+    v.list_boxes = (const rtk::DBoxF*)off(put(blob, hw.list_boxes));
     v.xforms = (const rtk::DXform*)off(put(blob, hw.xforms));
     v.media = (const rtk::DMedium*)off(put(blob, hw.media));
     v.materials = (const rtk::DMaterial*)off(put(blob, hw.materials));
@@ -393,7 +394,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
     fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
         fix(v.msph_mat), fix(v.planars), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
-        fix(v.remap_nm), fix(v.list_children), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
+        fix(v.remap_nm), fix(v.list_children), fix(v.list_boxes), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
         fix(v.texels), fix(v.perlin);
     d->view = v;
     d->tier = fw.tier;

@@ -191,6 +191,14 @@ struct Flattener {
         return b;
     }
 
+    static rtk::DBoxF boxf(const Box3& b) {
+        rtk::DBoxF r{};
+        for (int k = 0; k < 3; ++k) {
+            r.lo[k] = round_down(b.a[k].lo);
+            r.hi[k] = round_up(b.a[k].hi);
+        }
+        return r;
+    }
     void set_box(rtk::DNode& n, int which, const Box3& b) {
         auto& bx = n.slot[which].box;
         for (int k = 0; k < 3; ++k) {
@@ -428,8 +436,12 @@ struct Flattener {
                 std::vector<std::pair<uint32_t, uint32_t>> kids;
                 for (int c : o.children) kids.push_back(emit(c, in_boundary, xf_depth));
                 uint32_t start = (uint32_t)out.list_children.size();
-                for (auto& k : kids) out.list_children.push_back(k.first);
+                for (size_t i = 0; i < kids.size(); ++i) {
+                    out.list_children.push_back(kids[i].first);
+                    out.list_boxes.push_back(boxf(tight(o.children[i])));
+                }
                 out.list_children.push_back(REF_NONE_);
+                out.list_boxes.push_back(boxf(Box3::empty()));
                 // iterator form: popping (LIST,p) pushes (LIST,p+1) then walks child p
                 uint32_t need = 0;
                 for (size_t i = 0; i < kids.size(); ++i) {
@@ -705,7 +717,10 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
                 return set_error(RT_EUNSUPPORTED, "DiffuseLight wrapping Mix/DiffuseLight is not on the kernel path yet");
         }
     }
-    if (out.list_children.empty()) out.list_children.push_back(rtk::REF_NONE);
+    if (out.list_children.empty()) {
+        out.list_children.push_back(rtk::REF_NONE);
+        out.list_boxes.push_back(rtk::DBoxF{});
+    }
     return RT_OK;
 }
 

@@ -119,6 +119,7 @@ struct HostWorld {
     std::vector<rtk::DRemap> remaps;
     std::vector<rtk::DRemapNM> remap_nm;  // parallel to remaps when any normal map is used
     std::vector<uint32_t> list_children;
+    std::vector<rtk::DBoxF> list_boxes;  // parallel to list_children
     std::vector<rtk::DXform> xforms;
     std::vector<rtk::DMedium> media;
     std::vector<rtk::DMaterial> materials;

