@@ -75,6 +75,8 @@ extern "C" uint32_t rtk_stack_entries(int tier);
 extern "C" int rtk_basic_bvh4(void);
 // 1 if the mesh tier's kernel walks 4-wide BVH nodes with every child boxed
 extern "C" int rtk_mesh_bvh4(void);
+// 1 if the kernel runs the f32 quad / triangle pre-test (rt_planar_filter.h)
+extern "C" int rtk_planar_filter(void);
 extern "C" int rtk_full_bvh4(void);
 extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
                                        double* partial, unsigned long long* stats, float* out, uint8_t* srgb,

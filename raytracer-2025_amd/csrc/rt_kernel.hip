@@ -235,17 +235,36 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
     return true;
 }
 
+#ifndef RT_PLANAR_EARLY
+// 1: decide early, with the same outcome as the full test: t = num / denom
+// rounded is negative when num and denom have opposite signs (num != 0), so
+// t < tmin for tmin >= 0; with equal signs, |num| > tmax |denom| (1 + 2^-40)
+// puts the correctly rounded quotient above tmax (the product's two roundings
+// are 2^-52 apart from the margin) -- both without the f64 division; and alpha
+// out of [0, 1] rejects before beta.  Measured slower (A/B at 128 spp, min of
+// 4, r02h: C3 +4.7 %, C4 +3.6 %, C5 +2.7 %): the lanes of a wave take both
+// sides of every new branch, so no wave skips the division -- it only pays the
+// branches.  Kept as an option.
+#define RT_PLANAR_EARLY 0
+#endif
 // quad.rs:71-102 / triangle.rs:69-98
 __device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& r, double tmin, double tmax,
                                          double& t) {
     const D3 n = d3(P.f[0], P.f[1], P.f[2]);
     const double denom = dot(n, r.d);
     if (fabs(denom) < 1e-8) return false;
-    const double tt = (P.f[3] - dot(n, r.o)) / denom;
+    const double num = P.f[3] - dot(n, r.o);
+    if constexpr (RT_PLANAR_EARLY) {
+        const bool same = (num < 0.0) == (denom < 0.0);
+        if (!same && num != 0.0 && tmin >= 0.0) return false;
+        if (same && fabs(num) > (tmax * fabs(denom)) * (1.0 + 0x1p-40)) return false;
+    }
+    const double tt = num / denom;
     if (!(tt >= tmin && tt <= tmax)) return false;
     const D3 hv = (r.o + tt * r.d) - d3(P.f[4], P.f[5], P.f[6]);
     const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
     const double alpha = dot(w, cross(hv, v));
+    if (RT_PLANAR_EARLY && !(alpha >= 0.0 && alpha <= 1.0)) return false;
     const double beta = dot(w, cross(u, hv));
     if (!(alpha >= 0.0 && alpha <= 1.0 && beta >= 0.0 && beta <= 1.0)) return false;
     if (tri) {
@@ -254,6 +273,27 @@ __device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& 
     }
     t = tt;
     return true;
+}
+
+#ifndef RT_PLANAR_FILTER
+// 1: quads / triangles take the f32 pre-test (rt_planar_filter.h) before
+// planar_t.  Measured slower (A/B at 128 spp, min of 4: C4 +13 %, C5 +5 %,
+// C3 +2 %): a triangle reached through a hit box is rarely ruled out, and a
+// flat-tier quad's f32 test costs about what the f64 one does.  Kept as an
+// option with its CPU property test (tests/test_planar_filter_cpu.py).
+#define RT_PLANAR_FILTER 0
+#endif
+// planar_t behind the conservative f32 pre-test: the f64 record is read and
+// tested only when the f32 test cannot rule the primitive out.  The
+// pre-test's "behind the origin" rejection needs tmin >= 0 (a medium
+// boundary walk starts at -inf).
+__device__ __forceinline__ bool planar_t_filtered(const SceneView& S, uint32_t idx, bool tri, const Ray& r,
+                                                  double tmin, double tmax, float tmax_f, double& t) {
+    if constexpr (RT_PLANAR_FILTER) {
+        const double o[3] = {r.o.x, r.o.y, r.o.z}, d[3] = {r.d.x, r.d.y, r.d.z};
+        if (tmin >= 0.0 && planar_reject(S.planars_f[idx], make_prayf(o, d), tmax_f, tri)) return false;
+    }
+    return planar_t(S.planars[idx], tri, r, tmin, tmax, t);
 }
 
 // Transform::detransform (shapes.rs:80-84): R^-1 (v - offset) / scale
@@ -300,18 +340,25 @@ struct HitInfo {
 // the LDS part stays small enough for 4 blocks per CU.
 template <uint32_t CAP, bool OVF, uint32_t BLK>
 struct StackT {
-    uint2* base;
+    RT_LDS uint2* base;  // explicitly LDS: a select against ovf must not become a flat pointer
     RT_GLOBAL uint2* ovf;
     uint32_t stride;
+    // The overflow side moves the entry as one 64-bit word and the LDS side
+    // as a uint2: different instructions, so the optimizer cannot merge the
+    // two accesses into one through a phi of flat pointers (which also hit a
+    // gfx950 code-generation error on an LDS-to-flat cast in the flat tier).
     __device__ __forceinline__ void push(uint32_t sp, uint32_t ref, float t) {
-        const uint2 v = make_uint2(ref, __float_as_uint(t));
         if (OVF && sp >= CAP)
-            ovf[(sp - CAP) * stride] = v;
+            reinterpret_cast<RT_GLOBAL unsigned long long*>(ovf)[(sp - CAP) * stride] =
+                ((unsigned long long)__float_as_uint(t) << 32) | ref;
         else
-            base[sp * BLK] = v;
+            base[sp * BLK] = make_uint2(ref, __float_as_uint(t));
     }
     __device__ __forceinline__ uint2 at(uint32_t sp) const {
-        if (OVF && sp >= CAP) return ovf[(sp - CAP) * stride];
+        if (OVF && sp >= CAP) {
+            const unsigned long long v = reinterpret_cast<const RT_GLOBAL unsigned long long*>(ovf)[(sp - CAP) * stride];
+            return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        }
         return base[sp * BLK];
     }
 };
@@ -396,7 +443,13 @@ __device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t
 
 constexpr float NO_CULL = -__builtin_huge_valf();
 #ifndef RT_FLAT_LIST_BOXES
-#define RT_FLAT_LIST_BOXES 0  // 1: the flat tier tests list elements' f32 boxes first (C3 -4.6 %: not kept)
+// The flat tier tests the f32 box of a compound list element (a Transform, a
+// ConstantMedium, a nested list) before entering it, with the ray's f32 form
+// made on the spot: a ray that misses the box skips the element's whole
+// walk -- for C3's smoke box the two boundary walks of media_phase.  (Testing
+// every element's box, primitives included, with the f32 ray parked in LDS
+// was 4.6 % slower: a wall's box test costs what its exact test does.)
+#define RT_FLAT_LIST_BOXES 1
 #endif
 template <int TIER>
 constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXES; }
@@ -410,23 +463,6 @@ constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXE
 // (for a ConstantMedium: cannot enter its boundary there), so skipping it
 // keeps the list's closest hit -- the role a BVH node's boxes play, without
 // the BVH code.
-// Flat tier: the f32 ray of the walk lives in LDS ([3][block] float4 per
-// lane), read by the element box tests only -- 12 registers the walk's
-// other state needs more (152 B/lane of spills with it in registers).
-__device__ __forceinline__ void store_rayf(float4* p, const RayF& R) {
-    p[0] = make_float4(R.idl[0], R.idl[1], R.idl[2], R.idh[0]);
-    p[RT_BLOCK] = make_float4(R.idh[1], R.idh[2], R.nlo[0], R.nlo[1]);
-    p[2 * RT_BLOCK] = make_float4(R.nlo[2], R.nhi[0], R.nhi[1], R.nhi[2]);
-}
-__device__ __forceinline__ RayF load_rayf(const float4* p) {
-    const float4 a = p[0], b = p[RT_BLOCK], c = p[2 * RT_BLOCK];
-    RayF R;
-    R.idl[0] = a.x, R.idl[1] = a.y, R.idl[2] = a.z, R.idh[0] = a.w;
-    R.idh[1] = b.x, R.idh[2] = b.y, R.nlo[0] = b.z, R.nlo[1] = b.w;
-    R.nlo[2] = c.x, R.nhi[0] = c.y, R.nhi[1] = c.z, R.nhi[2] = c.w;
-    return R;
-}
-
 __device__ __forceinline__ bool list_box_hit(const SceneView& S, uint32_t li, const RayF& rf, float tmin_f,
                                              float c_f) {
     const RT_GLOBAL float4* bp = reinterpret_cast<const RT_GLOBAL float4*>(S.list_boxes + li);
@@ -512,7 +548,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             }
             case K_QUAD:
             case K_TRI:
-                if (planar_t(S.planars[idx], kind == K_TRI, r, tmin, cl.c, t)) {
+                if (planar_t_filtered(S, idx, kind == K_TRI, r, tmin, cl.c, cl.c_f, t)) {
                     cl.set(t);
                     found = true;
                 }
@@ -601,12 +637,9 @@ struct Trav {
 };
 
 template <int TIER>
-__device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, Trav<TIER>& T, float4* rfl) {
+__device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, Trav<TIER>& T) {
     T.r = wr;
-    if constexpr (flat_boxes<TIER>())
-        store_rayf(rfl, make_rayf(wr));
-    else
-        T.rf = make_rayf(wr);
+    T.rf = make_rayf(wr);
     T.a = len2(wr.d);
     T.inva = 1.0 / T.a;
     T.cl.c = __builtin_huge_val();
@@ -627,7 +660,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
 template <int TIER>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                           const Rng& rng, uint4* med, float4* rfl, Diag& dg) {
+                                           const Rng& rng, RT_LDS uint4* med, Diag& dg) {
     constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
@@ -657,7 +690,9 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         if (child == REF_NONE) return true;  // empty list
         const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
         if constexpr (flat_boxes<TIER>()) {
-            if (!list_box_hit(S, li, load_rayf(rfl), tmin_f, T.cl.c_f)) {
+            const uint32_t ck = ref_kind(child);
+            if (ck != K_SPHERE && ck != K_QUAD && ck != K_TRI && ck != K_MSPHERE &&
+                !list_box_hit(S, li, make_rayf(r), tmin_f, T.cl.c_f)) {
                 T.cur = nxt;
                 return true;
             }
@@ -695,7 +730,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         const double4 sp4 = S.spheres[idx];
         got = sphere_t_inv(d3(sp4.x, sp4.y, sp4.z), sp4.w, r, T.a, T.inva, tmin, T.cl.c, t);
     } else if constexpr (TIER == TIER_MESH) {
-        if (kind == K_TRI || kind == K_QUAD) got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, T.cl.c, t);
+        if (kind == K_TRI || kind == K_QUAD) got = planar_t_filtered(S, idx, kind == K_TRI, r, tmin, T.cl.c, T.cl.c_f, t);
     } else if constexpr (FULL) {
         switch (kind) {
             case K_MSPHERE: {
@@ -705,16 +740,13 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 break;
             }
             case K_QUAD:
-            case K_TRI: got = planar_t(S.planars[idx], kind == K_TRI, r, tmin, T.cl.c, t); break;
+            case K_TRI: got = planar_t_filtered(S, idx, kind == K_TRI, r, tmin, T.cl.c, T.cl.c_f, t); break;
             case K_XFORM: {
                 const DXform& X = S.xforms[idx];
                 stk.push(T.sp++, make_ref(K_POPXF, 0), NO_CULL);
                 T.xfs.set(T.nxf++, idx);
                 T.r = xf_ray(X, T.r);
-                if constexpr (flat_boxes<TIER>())
-                    store_rayf(rfl, make_rayf(T.r));
-                else
-                    T.rf = make_rayf(T.r);
+                T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
                 T.inva = 1.0 / T.a;
                 T.cur = X.child;
@@ -724,10 +756,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
                 --T.nxf;
                 T.r = wr;
                 for (uint32_t k = 0; k < T.nxf; ++k) T.r = xf_ray(S.xforms[T.xfs.get(k)], T.r);
-                if constexpr (flat_boxes<TIER>())
-                    store_rayf(rfl, make_rayf(T.r));
-                else
-                    T.rf = make_rayf(T.r);
+                T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
                 T.inva = 1.0 / T.a;
                 break;
@@ -761,7 +790,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
 // against the walk's closest t; the walk's stack is free again.
 template <int TIER>
 __device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                            const Rng& rng, const uint4* med) {
+                                            const Rng& rng, const RT_LDS uint4* med) {
     for (uint32_t k = 0; k < T.nmed; ++k) {
         const uint4 e = med[k * RT_BLOCK];
         Ray r = wr;
@@ -799,14 +828,14 @@ constexpr uint32_t NODE_LDS_CAP = RT_NODE_LDS_BYTES / sizeof(DNode4);
 // spheres; larger sphere worlds run the mesh tier).  A per-wave
 // fallback to global reads for larger trees cost 88 B/lane of scratch at the
 // 128-VGPR budget.
-__device__ __forceinline__ Node4Rows load_node4(const float4* nl, uint32_t idx) {
-    const float4* np = nl + idx * 7u;
+__device__ __forceinline__ Node4Rows load_node4(const RT_LDS float4* nl, uint32_t idx) {
+    const RT_LDS float4* np = nl + idx * 7u;
     return Node4Rows{np[0], np[1], np[2], np[3], np[4], np[5], np[6]};
 }
 // visit4 on node rows already loaded
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
-                                                float& c_f, Stack& stk, uint32_t& sp, uint16_t* pq, uint32_t& pn) {
+                                                float& c_f, Stack& stk, uint32_t& sp, RT_LDS uint16_t* pq, uint32_t& pn) {
     const float4 lx = nr.lx, ly = nr.ly, lz = nr.lz, hx = nr.hx, hy = nr.hy, hz = nr.hz, rq = nr.rq;
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
@@ -906,7 +935,7 @@ __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t id
 // trace_step's walk (A/B renders: RMSE 0).
 template <class Stack>
 __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Trav<TIER_BASIC>& T, Stack& stk,
-                                            uint16_t* pq, const float4* nl, Diag& dg) {
+                                            RT_LDS uint16_t* pq, const RT_LDS float4* nl, Diag& dg) {
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
     constexpr uint32_t ROOM = RT_PEND_CAP - 4;  // a visit queues at most 4
@@ -1516,10 +1545,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
     __shared__ uint2 stack_lds[STACK * BLK];
     __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
-    uint4* med = media_lds + threadIdx.x;
+    RT_LDS uint4* med = (RT_LDS uint4*)(media_lds + threadIdx.x);
     __shared__ uint16_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * BLK : 1];
-    uint16_t* pq = pend_lds + threadIdx.x;
-    StackFor<TIER> stk{stack_lds + threadIdx.x,
+    RT_LDS uint16_t* pq = (RT_LDS uint16_t*)(pend_lds + threadIdx.x);
+    StackFor<TIER> stk{(RT_LDS uint2*)(stack_lds + threadIdx.x),
                        P->stack_ovf + (uint64_t)blockIdx.x * BLK + threadIdx.x, gridDim.x * BLK};
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
     // 241 nodes for C1/C2), read by every node visit instead of global memory.
@@ -1537,10 +1566,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
     __shared__ double pstate_lds[LDS_STATE ? 9 * RT_BLOCK : 1];
     __shared__ uint4 pitem_lds[LDS_STATE ? RT_BLOCK : 1];
-    double* pst = pstate_lds + threadIdx.x;
-    uint4* pit = pitem_lds + threadIdx.x;
-    __shared__ float4 rayf_lds[flat_boxes<TIER>() ? 3 * RT_BLOCK : 1];
-    float4* rfl = rayf_lds + threadIdx.x;
+    RT_LDS double* pst = (RT_LDS double*)(pstate_lds + threadIdx.x);
+    RT_LDS uint4* pit = (RT_LDS uint4*)(pitem_lds + threadIdx.x);
 
     Rng rng;
     rng.k0 = F.key0;
@@ -1640,7 +1667,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         if (!walking) {
             rng.begin(vertex);
             ++n_rays;
-            trace_begin<TIER>(S, ray, T, rfl);
+            trace_begin<TIER>(S, ray, T);
             walking = true;
         }
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
@@ -1649,10 +1676,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                             : TIER == TIER_FULL ? RT_SHADE_BATCH_FULL : RT_SHADE_BATCH_FLAT;
         auto step = [&]() -> bool {
             if constexpr (TIER == TIER_BASIC && RT_BVH4) {
-                return trace4_step(S, ray, T, stk, pq, node_lds, dg);
+                return trace4_step(S, ray, T, stk, pq, (const RT_LDS float4*)node_lds, dg);
             } else {
                 RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
-                return trace_step<TIER>(S, ray, T, stk, rng, med, rfl, dg);
+                return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
             }
         };
         if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
@@ -1865,6 +1892,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 }
 
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
+extern "C" int rtk_planar_filter(void) { return RT_PLANAR_FILTER; }
 extern "C" int rtk_block_threads(int tier) { return tier == rtk::TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }
 extern "C" int rtk_full_bvh4(void) { return RT_FULL_BVH4; }

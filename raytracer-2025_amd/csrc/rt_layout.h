@@ -18,6 +18,7 @@
 //    test reads in one 128-B record and area/material apart;
 //  - materials/textures are small tables read once per bounce.
 #pragma once
+#include "rt_planar_filter.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,8 +27,10 @@
 // so serialises with the LDS traversal stack).
 #if defined(__HIP_DEVICE_COMPILE__)
 #define RT_GLOBAL __attribute__((address_space(1)))
+#define RT_LDS __attribute__((address_space(3)))
 #else
 #define RT_GLOBAL
+#define RT_LDS
 #endif
 
 namespace rtk {
@@ -194,6 +197,7 @@ struct SceneView {
     const RT_GLOBAL double4* msph_dir;       // {c2-c1, 0}
     const RT_GLOBAL int32_t* msph_mat;
     const RT_GLOBAL DPlanar* planars;        // quads then triangles share the record
+    const RT_GLOBAL PlanarF* planars_f;      // their f32 pre-test records (rt_planar_filter.h)
     const RT_GLOBAL double* planar_area;
     const RT_GLOBAL int32_t* planar_mat;
     const RT_GLOBAL int32_t* planar_remap;   // index into remaps, -1 = plain Triangle/Quad

@@ -290,6 +290,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.msph_dir = (const double4*)off(put(blob, hw.msph_dir));
     v.msph_mat = (const int32_t*)off(put(blob, hw.msph_mat));
     v.planars = (const rtk::DPlanar*)off(put(blob, hw.planars));
+    v.planars_f = (const rtk::PlanarF*)off(put(blob, hw.planars_f));
     v.planar_area = (const double*)off(put(blob, hw.planar_area));
     v.planar_mat = (const int32_t*)off(put(blob, hw.planar_mat));
     v.planar_remap = (const int32_t*)off(put(blob, hw.planar_remap));
@@ -393,7 +394,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     rtk::SceneView v = fw.rel;
     auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
     fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
-        fix(v.msph_mat), fix(v.planars), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
+        fix(v.msph_mat), fix(v.planars), fix(v.planars_f), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
         fix(v.remap_nm), fix(v.list_children), fix(v.list_boxes), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
         fix(v.texels), fix(v.perlin);
     d->view = v;

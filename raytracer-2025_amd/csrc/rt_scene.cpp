@@ -1,5 +1,6 @@
 // rt_scene.cpp -- builder half of the C ABI (include/rt_mi355x.h) and the
 // world flattener.  Host code only; the device half is rt_render.hip.
+#include "rt_kernel.h"
 #include "rt_scene.hpp"
 
 #include <algorithm>
@@ -120,6 +121,21 @@ float round_up(double x) {
     if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
     return f;
 }
+// The f32 pre-test record of a quad / triangle (rt_planar_filter.h): n, D,
+// Q rounded to nearest, a = v x w and b = w x u from the f64 vectors, and
+// the error-bound magnitudes rounded up.
+rtk::PlanarF planar_f(const Obj& o) {
+    rtk::PlanarF F{};
+    const V3 a = cross(o.v, o.w), b = cross(o.w, o.u);
+    auto l1 = [](V3 x) { return std::fabs(x.x) + std::fabs(x.y) + std::fabs(x.z); };
+    F.n[0] = (float)o.normal.x, F.n[1] = (float)o.normal.y, F.n[2] = (float)o.normal.z, F.D = (float)o.D;
+    F.q[0] = (float)o.anchor.x, F.q[1] = (float)o.anchor.y, F.q[2] = (float)o.anchor.z;
+    F.g = round_up(8.0 * l1(o.anchor) + 2.0 * std::fabs(o.D));
+    F.a[0] = (float)a.x, F.a[1] = (float)a.y, F.a[2] = (float)a.z, F.sa = round_up(l1(a));
+    F.b[0] = (float)b.x, F.b[1] = (float)b.y, F.b[2] = (float)b.z, F.sb = round_up(l1(b));
+    return F;
+}
+
 double half_area(const Box3& b) {
     double dx = std::fmax(b.a[0].hi - b.a[0].lo, 0.0), dy = std::fmax(b.a[1].hi - b.a[1].lo, 0.0),
            dz = std::fmax(b.a[2].hi - b.a[2].lo, 0.0);
@@ -370,6 +386,7 @@ struct Flattener {
                                 o.u.y,      o.u.z,      o.v.x,      o.v.y, o.v.z,      o.w.x,      o.w.y,      o.w.z};
                 std::memcpy(p.f, f, sizeof f);
                 out.planars.push_back(p);
+                if (rtk_planar_filter()) out.planars_f.push_back(planar_f(o));
                 out.planar_area.push_back(o.area);
                 out.planar_mat.push_back(o.mat);
                 if (o.remap) {

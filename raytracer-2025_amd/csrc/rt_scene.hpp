@@ -113,6 +113,7 @@ struct HostWorld {
     std::vector<double4> msph_center, msph_dir;
     std::vector<int32_t> msph_mat;
     std::vector<rtk::DPlanar> planars;
+    std::vector<rtk::PlanarF> planars_f;  // parallel to planars
     std::vector<double> planar_area;
     std::vector<int32_t> planar_mat;
     std::vector<int32_t> planar_remap;
