@@ -65,6 +65,14 @@ int32_t rt_tex_checker(rt_scene* s, double scale, int32_t even_tex, int32_t odd_
  * missing file: value() is cyan (texture.rs:167-169).  linear_interp selects
  * ImageInterpMethod::Linear (new_raw_image) instead of None. */
 int32_t rt_tex_image(rt_scene* s, uint32_t width, uint32_t height, const float* rgba, int32_t linear_interp);
+/* ImageTexture::new / new_raw_image (texture.rs:82-97) with the file path
+ * given directly (the reference joins RTW_IMAGES or ./assets, image.rs:21-46):
+ * the library decodes PNG (rt_png.hpp: the image crate's into_rgba32f, then
+ * the sRGB EOTF unless raw, image.rs:63-82).  A file that is missing or fails
+ * to decode is the reference's Image::EMPTY (cyan); another format, or an
+ * interlaced PNG, is RT_EUNSUPPORTED.  raw != 0: no sRGB conversion
+ * (new_raw_image); linear_interp selects ImageInterpMethod::Linear. */
+int32_t rt_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t linear_interp);
 /* NoiseTexture::new (texture.rs:183-188).  Perlin tables are drawn from
  * SplitMix64(seed) in the order of perlin.rs:16-36. */
 int32_t rt_tex_noise(rt_scene* s, double scale, uint64_t seed);
@@ -84,6 +92,9 @@ int32_t rt_mat_diffuse_light(rt_scene* s, int32_t tex, int32_t inner_mat);
 int32_t rt_mat_isotropic(rt_scene* s, int32_t tex);                        /* Isotropic::new 193-197 */
 int32_t rt_mat_transparent(rt_scene* s);                                   /* Transparent 209-218 */
 int32_t rt_mat_mix(rt_scene* s, int32_t mat1, int32_t mat2, double ratio); /* Mix::new 227-233 */
+/* Mix::from_image (material.rs:235-247): ratio = the image texture's alpha at
+ * (u, v) (ImageTexture::alpha, texture.rs:99-106: 1 for a missing image) */
+int32_t rt_mat_mix_image(rt_scene* s, int32_t mat1, int32_t mat2, int32_t image_tex);
 
 /* ---- Hittables ------------------------------------------------------------ */
 /* Sphere::new (shapes/sphere.rs:25-35) */
@@ -113,9 +124,10 @@ int32_t rt_constant_medium_new(rt_scene* s, int32_t boundary, double density, in
  * MTL and map_* paths resolve against the OBJ's directory).  tobj
  * GPU_LOAD_OPTIONS semantics; one BVH per loaded model, each triangle under a
  * RemappedMaterial (vertex normals + texture coordinates, obj.rs:20-81).
- * vanilla != 0: Metal / Dielectric from Pm / Tf (obj.rs:289-298); Disney
- * materials, normal maps and image maps -> RT_EUNSUPPORTED.  Returns a
- * Hittables object (possibly empty). */
+ * vanilla != 0: Metal / Dielectric from Pm / Tf (obj.rs:289-298); image maps
+ * (map_Kd, map_Ke, map_d, map_Bump / normal) are decoded as rt_tex_image_file
+ * does (obj.rs:212-345: map_d -> Mix::from_image(Transparent, mat)); Disney
+ * materials -> RT_EUNSUPPORTED.  Returns a Hittables object (possibly empty). */
 int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla);
 
 /* Quaternion::from_axis_angle / from_euler (utils/quaternion.rs:23-53), host helpers */

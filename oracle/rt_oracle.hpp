@@ -603,17 +603,25 @@ struct Transparent : Material {  // material.rs:209-218
         return ray_record(Color(1.0, 1.0, 1.0), Ray(rec.p, r_in.dir, r_in.time));
     }
 };
-struct Mix : Material {  // material.rs:220-268 (constant ratio form, Mix::new)
+struct Mix : Material {  // material.rs:220-268: Mix::new (constant) or Mix::from_image (alpha)
     std::shared_ptr<Material> mat1, mat2;
     double ratio;
+    std::shared_ptr<ImageTexture> ratio_tex;  // Mix::from_image (material.rs:235-247), else null
     Mix(std::shared_ptr<Material> a, std::shared_ptr<Material> b, double r)
         : mat1(std::move(a)), mat2(std::move(b)), ratio(r) {}
+    Mix(std::shared_ptr<Material> a, std::shared_ptr<Material> b, std::shared_ptr<ImageTexture> t)
+        : mat1(std::move(a)), mat2(std::move(b)), ratio(0.0), ratio_tex(std::move(t)) {}
+    double get_ratio(const HitRecord& rec) const {  // material.rs:249-251
+        return ratio_tex ? ratio_tex->alpha(rec.u, rec.v) : ratio;
+    }
     std::optional<ScatterRecord> scatter(const Ray& r_in, const HitRecord& rec) const override {
-        if (Random::f64() > ratio) return mat1->scatter(r_in, rec);
+        const double r = get_ratio(rec);
+        if (Random::f64() > r) return mat1->scatter(r_in, rec);
         return mat2->scatter(r_in, rec);
     }
     Color emitted(const Ray& r_in, const HitRecord& rec) const override {
-        return mat1->emitted(r_in, rec) * (1.0 - ratio) + mat2->emitted(r_in, rec) * ratio;
+        const double r = get_ratio(rec);
+        return mat1->emitted(r_in, rec) * (1.0 - r) + mat2->emitted(r_in, rec) * r;
     }
 };
 

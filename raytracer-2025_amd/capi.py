@@ -86,6 +86,7 @@ SIGNATURES = {
     "tex_solid": (_I, [_P, _DP]),
     "tex_checker": (_I, [_P, _D, _I, _I]),
     "tex_image": (_I, [_P, _U, _U, C.POINTER(C.c_float), _I]),
+    "tex_image_file": (_I, [_P, C.c_char_p, _I, _I]),
     "tex_noise": (_I, [_P, _D, C.c_uint64]),
     "tex_sky_gradient": (_I, [_P, _DP, _DP]),
     "mat_empty": (_I, [_P]),
@@ -96,6 +97,7 @@ SIGNATURES = {
     "mat_isotropic": (_I, [_P, _I]),
     "mat_transparent": (_I, [_P]),
     "mat_mix": (_I, [_P, _I, _I, _D]),
+    "mat_mix_image": (_I, [_P, _I, _I, _I]),
     "sphere": (_I, [_P, _DP, _D, _I]),
     "sphere_moving": (_I, [_P, _DP, _DP, _D, _I]),
     "quad": (_I, [_P, _DP, _DP, _DP, _I]),

@@ -110,6 +110,40 @@ __device__ void image_pixel(const SceneView& S, const DTexture& t, int64_t x, in
     out[3] = px[3];
 }
 
+// ImageTexture::get_pixel (texture.rs:109-158): nearest or bilinear, u / v
+// wrapped by x - floor(x), v flipped; t.b != 0 (a loaded image)
+__device__ __forceinline__ void image_rgba(const SceneView& S, const DTexture& t, double u, double v, float px[4]) {
+    const double uu = u - floor(u);
+    const double vv = 1.0 - (v - floor(v));
+    if (!t.c) {
+        const uint32_t i = (uint32_t)(uu * (double)t.a), j = (uint32_t)(vv * (double)t.b);
+        image_pixel(S, t, i, j, px);
+        return;
+    }
+    const double x = uu * (double)t.a - 0.5, y = vv * (double)t.b - 0.5;
+    const uint32_t x0 = (uint32_t)fmax(floor(x), 0.0), y0 = (uint32_t)fmax(floor(y), 0.0);
+    const uint32_t x1 = min(x0 + 1, (uint32_t)t.a - 1), y1 = min(y0 + 1, (uint32_t)t.b - 1);
+    const float dx = (float)(x - (double)x0), dy = (float)(y - (double)y0);
+    float p00[4], p10[4], p01[4], p11[4];
+    image_pixel(S, t, x0, y0, p00);
+    image_pixel(S, t, x1, y0, p10);
+    image_pixel(S, t, x0, y1, p01);
+    image_pixel(S, t, x1, y1, p11);
+    for (int c = 0; c < 4; ++c) {
+        const float v0 = p00[c] * (1.0f - dx) + p10[c] * dx;
+        const float v1 = p01[c] * (1.0f - dx) + p11[c] * dx;
+        px[c] = v0 * (1.0f - dy) + v1 * dy;
+    }
+}
+// ImageTexture::alpha (texture.rs:99-106): 1 for a missing image
+__device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double u, double v) {
+    const DTexture& t = S.textures[tid];
+    if (t.b == 0) return 1.0;
+    float px[4];
+    image_rgba(S, t, u, v, px);
+    return (double)px[3];
+}
+
 template <bool FULL>
 __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
     for (int guard = 0; guard < 16; ++guard) {
@@ -132,28 +166,8 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
           switch (t.type) {
             case T_IMAGE: {
                 if (t.b == 0) return d3(0.0, 1.0, 1.0);  // texture.rs:167-169
-                const double uu = u - floor(u);
-                const double vv = 1.0 - (v - floor(v));
                 float px[4];
-                if (!t.c) {
-                    const uint32_t i = (uint32_t)(uu * (double)t.a), j = (uint32_t)(vv * (double)t.b);
-                    image_pixel(S, t, i, j, px);
-                } else {
-                    const double x = uu * (double)t.a - 0.5, y = vv * (double)t.b - 0.5;
-                    const uint32_t x0 = (uint32_t)fmax(floor(x), 0.0), y0 = (uint32_t)fmax(floor(y), 0.0);
-                    const uint32_t x1 = min(x0 + 1, (uint32_t)t.a - 1), y1 = min(y0 + 1, (uint32_t)t.b - 1);
-                    const float dx = (float)(x - (double)x0), dy = (float)(y - (double)y0);
-                    float p00[4], p10[4], p01[4], p11[4];
-                    image_pixel(S, t, x0, y0, p00);
-                    image_pixel(S, t, x1, y0, p10);
-                    image_pixel(S, t, x0, y1, p01);
-                    image_pixel(S, t, x1, y1, p11);
-                    for (int c = 0; c < 4; ++c) {
-                        const float v0 = p00[c] * (1.0f - dx) + p10[c] * dx;
-                        const float v1 = p01[c] * (1.0f - dx) + p11[c] * dx;
-                        px[c] = v0 * (1.0f - dy) + v1 * dy;
-                    }
-                }
+                image_rgba(S, t, u, v, px);
                 return d3(px[0], px[1], px[2]);
             }
             case T_NOISE: {
@@ -1288,6 +1302,35 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 #define RT_HOIST_DRAWS 1
 #endif
 
+// ---- general materials (tier FULL_GL): DiffuseLight / Mix wrappers nested
+// up to RT_MAT_DEPTH levels (rt_scene.cpp checks), Mix::from_image ratios.
+constexpr int RT_MAT_DEPTH = 4;
+// Mix::get_ratio (material.rs:249-251): the constant, or the image's alpha
+__device__ __forceinline__ double mix_ratio(const SceneView& S, const DMaterial& M, double u, double v) {
+    return M.tex >= 0 ? tex_alpha(S, M.tex, u, v) : M.fuzz;
+}
+// Material::emitted of a wrapper tree: DiffuseLight = its texture + the
+// wrapped material's emission (material.rs:171-178), Mix = mat1 * (1 - r) +
+// mat2 * r (material.rs:262-266), anything else BLACK
+template <int D>
+__device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p) {
+    const DMaterial& M = S.materials[mid];
+    if (M.type == M_DIFFUSE_LIGHT) {
+        const D3 self = tex_value<true>(S, M.tex, u, v, p);
+        D3 inner = d3(0.0, 0.0, 0.0);
+        if constexpr (D > 0)
+            if (M.inner >= 0) inner = emitted_tree<D - 1>(S, M.inner, u, v, p);
+        return self + inner;
+    }
+    if constexpr (D > 0) {
+        if (M.type == M_MIX) {
+            const double r = mix_ratio(S, M, u, v);
+            return ((1.0 - r) * emitted_tree<D - 1>(S, M.inner, u, v, p)) + (r * emitted_tree<D - 1>(S, M.inner2, u, v, p));
+        }
+    }
+    return d3(0.0, 0.0, 0.0);
+}
+
 // ------------------------------------------------------------------ one ray_color level
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
@@ -1327,7 +1370,19 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
         xi1 = rng.next(ovf);
         sincos(2.0 * PI * xi0, &sn0, &cs0);
     }
-    if constexpr (FULL) {
+    if constexpr (TIER == TIER_FULL_GL) {
+        if (M.flags & MF_EMISSIVE) L = L + beta * emitted_tree<RT_MAT_DEPTH>(S, rec.mat, rec.u, rec.v, rec.p);
+        // the wrappers' scatter: DiffuseLight -> its material or None, Mix -> one draw (material.rs:180-185, 254-260)
+        for (int k = 0; k < RT_MAT_DEPTH && (M.type == M_DIFFUSE_LIGHT || M.type == M_MIX); ++k) {
+            if (M.type == M_DIFFUSE_LIGHT) {
+                if (M.inner < 0) return true;
+                M = S.materials[M.inner];
+            } else {
+                M = S.materials[rng.next(ovf) > mix_ratio(S, M, rec.u, rec.v) ? M.inner : M.inner2];
+            }
+        }
+        if (M.type == M_DIFFUSE_LIGHT) return true;  // a plain light at the last level
+    } else if constexpr (FULL) {
         // emitted (material.rs:30-33, 171-178, 262-266)
         if (M.flags & MF_EMISSIVE) {
             D3 em;
@@ -1885,7 +1940,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const float* __res
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
     const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL |
                           rtk::F_NORMALMAP;
-    if (features & rtk::F_GENLIGHTS) return rtk::TIER_FULL_GL;
+    if (features & rtk::F_GENERAL) return rtk::TIER_FULL_GL;
     if (features & full) return rtk::TIER_FULL;
     if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;

@@ -229,7 +229,8 @@ enum : uint32_t {
     F_TEXFULL = 32u,  // image / noise textures
     F_MATFULL = 64u,  // DiffuseLight, Isotropic, Transparent, Mix
     F_REMAP = 128u,   // OBJ triangles with RemappedMaterial
-    F_GENLIGHTS = 512u,  // lights beyond a primitive or a flat list of static primitives (tier FULL_GL)
+    F_GENERAL = 512u,  // tier FULL_GL: lights beyond a flat list of static primitives, nested
+                       // DiffuseLight / Mix wrappers, Mix::from_image ratios
     F_NORMALMAP = 256u,  // ... with a normal map (full tier: image textures)
 };
 

@@ -22,6 +22,7 @@
 #include <fstream>
 #include <map>
 #include <sstream>
+#include <tuple>
 #include <unordered_map>
 
 #include "../../include/rt_mi355x.h"
@@ -236,12 +237,22 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
         if (mtl_failed) mtls.clear();
         // load_materials (obj.rs:212-345)
         std::vector<int32_t> mats, normal_maps;
+        // ImageTexture::new(prefix/file) / new_raw_image: decoded once per
+        // (file, raw, interpolation) and shared (a missing file reads as cyan)
+        std::map<std::tuple<std::string, int, int>, int32_t> images;
+        auto image_tex = [&](const std::string& file, bool raw, bool linear) -> int32_t {
+            auto key = std::make_tuple(file, (int)raw, (int)linear);
+            auto it = images.find(key);
+            if (it != images.end()) return it->second;
+            const int32_t h = rt_tex_image_file(s, (dir + "/" + file).c_str(), raw, linear);
+            if (h >= 0) images[key] = h;
+            return h;
+        };
         for (const MtlRec& m : mtls) {
             int32_t base_tex;
             if (!m.diffuse_texture.empty()) {
-                if (file_exists(dir + "/" + m.diffuse_texture))
-                    return set_error(RT_EUNSUPPORTED, "map_Kd images must be decoded by the caller (rt_tex_image)");
-                base_tex = rt_tex_image(s, 0, 0, nullptr, 0);  // missing file: cyan (texture.rs:167-169)
+                base_tex = image_tex(m.diffuse_texture, false, false);
+                if (base_tex < 0) return base_tex;
             } else if (m.has_diffuse) {
                 base_tex = rt_tex_solid(s, m.diffuse);
             } else {
@@ -258,9 +269,18 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
             }
             int32_t mat;
             if (vanilla && metallic == 1.0) {
+                // Metal::new(base_color.value(0, 0, ZERO), Pr): an image's pixel
+                // at u = 0, v = 0 -> (0, height) clamped to the last row
+                // (texture.rs:109-118, image.rs:63-82); a missing one is cyan
                 const TexRec& t = s->texs[base_tex];
-                const double cyan[3] = {0.0, 1.0, 1.0};
-                mat = rt_mat_metal(s, t.type == rtk::T_SOLID ? t.color : cyan, roughness);
+                double albedo[3] = {0.0, 1.0, 1.0};
+                if (t.type == rtk::T_SOLID) {
+                    for (int k = 0; k < 3; ++k) albedo[k] = t.color[k];
+                } else if (t.h != 0) {
+                    const float* px = &s->texels[t.texel_offset + (size_t)(t.h - 1) * t.w * 4];
+                    for (int k = 0; k < 3; ++k) albedo[k] = (double)px[k];
+                }
+                mat = rt_mat_metal(s, albedo, roughness);
             } else if (vanilla && spec_trans == 1.0) {
                 mat = rt_mat_dielectric(s, base_tex, ior);
             } else {
@@ -268,10 +288,16 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
             }
             std::vector<double> ke = params(m, "Ke");
             if (ke.size() == 3) mat = rt_mat_diffuse_light(s, rt_tex_solid(s, ke.data()), mat);
-            if (m.unknown.count("map_Ke"))
-                return set_error(RT_EUNSUPPORTED, "map_Ke emission images are not on the kernel path");
-            if (!m.dissolve_texture.empty())
-                return set_error(RT_EUNSUPPORTED, "map_d dissolve images (Mix::from_image) are not on the kernel path");
+            if (m.unknown.count("map_Ke")) {  // obj.rs:319-323
+                const int32_t et = image_tex(m.unknown.at("map_Ke"), false, false);
+                if (et < 0) return et;
+                mat = rt_mat_diffuse_light(s, et, mat);
+            }
+            if (!m.dissolve_texture.empty()) {  // obj.rs:325-332: Mix::from_image(Transparent, mat, tex)
+                const int32_t dt = image_tex(m.dissolve_texture, false, false);
+                if (dt < 0) return dt;
+                mat = rt_mat_mix_image(s, rt_mat_transparent(s), mat, dt);
+            }
             if (m.has_dissolve && m.dissolve < 1.0) mat = rt_mat_mix(s, rt_mat_transparent(s), mat, m.dissolve);
             if (mat < 0) return mat;
             mats.push_back(mat);
@@ -286,9 +312,8 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
                     while (is >> part) last = part;
                     if (!last.empty()) name = last;
                 }
-                if (file_exists(dir + "/" + name))
-                    return set_error(RT_EUNSUPPORTED, "normal-map images must be decoded by the caller (rt_tex_image)");
-                ntex = rt_tex_image(s, 0, 0, nullptr, 0);
+                ntex = image_tex(name, true, true);
+                if (ntex < 0) return ntex;
             }
             normal_maps.push_back(ntex);
         }

@@ -1,6 +1,7 @@
 // rt_scene.cpp -- builder half of the C ABI (include/rt_mi355x.h) and the
 // world flattener.  Host code only; the device half is rt_render.hip.
 #include "rt_kernel.h"
+#include "rt_png.hpp"
 #include "rt_scene.hpp"
 
 #include <algorithm>
@@ -659,7 +660,7 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         std::string lerr;
         const int lk = light_tree(s, lights, 0, lerr);
         if (lk < 0) return set_error(lk, lerr);
-        if (lk == 2) out.features |= rtk::F_GENLIGHTS;
+        if (lk == 2) out.features |= rtk::F_GENERAL;
         F.no_collapse = true;
         F.memo.erase(lights);
         auto Lr = F.emit(lights, false, 0);
@@ -718,21 +719,32 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
             m.type == rtk::M_MIX)
             out.features |= rtk::F_MATFULL;
     }
+    // Wrapper materials (DiffuseLight with a material, Mix): the C3 / C5 tiers
+    // take one level whose Mix ratio is a constant; deeper trees and
+    // Mix::from_image ratios run the FULL_GL tier (rt_kernel.hip emitted_tree),
+    // up to RT_MAT_DEPTH (4) wrapper levels.
+    std::function<int(int)> wrap_depth = [&](int mid) -> int {
+        const rtk::DMaterial& m = out.materials[mid];
+        if (m.type == rtk::M_MIX) return 1 + std::max(wrap_depth(m.inner), wrap_depth(m.inner2));
+        if (m.type == rtk::M_DIFFUSE_LIGHT && m.inner >= 0) return 1 + wrap_depth(m.inner);
+        return 0;
+    };
     for (size_t i = 0; i < out.materials.size(); ++i) {
         if (!mat_used[i]) continue;
         const rtk::DMaterial& m = out.materials[i];
-        if (m.type == rtk::M_MIX) {
+        const int depth = wrap_depth((int)i);
+        if (depth > 4) return set_error(RT_EUNSUPPORTED, "DiffuseLight / Mix wrappers nested deeper than 4 levels");
+        bool general = m.type == rtk::M_MIX && m.tex >= 0;
+        if (m.type == rtk::M_MIX)
             for (int sub : {m.inner, m.inner2}) {
-                int st = out.materials[sub].type;
-                if (st == rtk::M_MIX || (st == rtk::M_DIFFUSE_LIGHT && out.materials[sub].inner >= 0))
-                    return set_error(RT_EUNSUPPORTED, "Mix of Mix / of DiffuseLight-with-material is not on the kernel path yet");
+                const int st = out.materials[sub].type;
+                if (st == rtk::M_MIX || (st == rtk::M_DIFFUSE_LIGHT && out.materials[sub].inner >= 0)) general = true;
             }
-        }
         if (m.type == rtk::M_DIFFUSE_LIGHT && m.inner >= 0) {
-            int st = out.materials[m.inner].type;
-            if (st == rtk::M_MIX || st == rtk::M_DIFFUSE_LIGHT)
-                return set_error(RT_EUNSUPPORTED, "DiffuseLight wrapping Mix/DiffuseLight is not on the kernel path yet");
+            const int st = out.materials[m.inner].type;
+            if (st == rtk::M_MIX || st == rtk::M_DIFFUSE_LIGHT) general = true;
         }
+        if (general) out.features |= rtk::F_GENERAL;
     }
     if (out.list_children.empty()) {
         out.list_children.push_back(rtk::REF_NONE);
@@ -833,6 +845,15 @@ int32_t rt_tex_image(rt_scene* s, uint32_t w, uint32_t h, const float* rgba, int
     t.texel_offset = s->texels.size();
     if (w) s->texels.insert(s->texels.end(), rgba, rgba + (size_t)w * h * 4);
     return push_tex(s, t);
+}
+int32_t rt_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t linear) {
+    if (!s || !path) return set_error(RT_EINVAL, "null argument");
+    uint32_t w = 0, h = 0;
+    std::vector<float> px;
+    std::string err;
+    const rtpng::Status st = rtpng::load(path, raw != 0, w, h, px, err);
+    if (st == rtpng::UNSUPPORTED) return set_error(RT_EUNSUPPORTED, err);
+    return rt_tex_image(s, w, h, px.empty() ? nullptr : px.data(), linear);  // MISSING: 0 x 0, cyan
 }
 int32_t rt_tex_noise(rt_scene* s, double scale, uint64_t seed) {
     if (!s) return set_error(RT_EINVAL, "null argument");
@@ -941,6 +962,19 @@ int32_t rt_mat_mix(rt_scene* s, int32_t m1, int32_t m2, double ratio) {
     m.inner = m1;
     m.inner2 = m2;
     m.param = ratio;
+    return push_mat(s, m);
+}
+
+int32_t rt_mat_mix_image(rt_scene* s, int32_t m1, int32_t m2, int32_t tex) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    if (!mat_ok(s, m1) || !mat_ok(s, m2)) return set_error(RT_EHANDLE, "unknown material");
+    if (!tex_ok(s, tex) || s->texs[tex].type != rtk::T_IMAGE)
+        return set_error(RT_EHANDLE, "Mix::from_image takes an ImageTexture");
+    MatRec m{};
+    m.type = rtk::M_MIX;
+    m.inner = m1;
+    m.inner2 = m2;
+    m.tex = tex;  // ratio = tex.alpha(u, v, p) (material.rs:237-247, texture.rs:99-106)
     return push_mat(s, m);
 }
 

@@ -107,6 +107,12 @@ class Scene:
         ptr = a.ctypes.data_as(C.POINTER(C.c_float))
         return Texture(self, self._c(self.api.tex_image(self.s, w, h, ptr, int(linear_interp))))
 
+    def ImageTexture_file(self, path, raw=False, linear_interp=None):
+        """ImageTexture::new(file) / new_raw_image(file) (texture.rs:82-97) with
+        the path given directly; PNG decoded by the library (missing -> cyan)."""
+        interp = raw if linear_interp is None else linear_interp
+        return Texture(self, self._c(self.api.tex_image_file(self.s, os.fsencode(path), int(raw), int(interp))))
+
     def NoiseTexture(self, scale, seed=0):
         return Texture(self, self._c(self.api.tex_noise(self.s, float(scale), int(seed))))
 
@@ -137,6 +143,10 @@ class Scene:
 
     def Mix(self, mat1, mat2, ratio):
         return Material(self, self._c(self.api.mat_mix(self.s, mat1.h, mat2.h, float(ratio))))
+
+    def Mix_from_image(self, mat1, mat2, image_tex):
+        """Mix::from_image (material.rs:235-247): ratio = the texture's alpha."""
+        return Material(self, self._c(self.api.mat_mix_image(self.s, mat1.h, mat2.h, image_tex.h)))
 
     # ---- hittables
     def Sphere(self, center, radius, mat):

@@ -6,6 +6,7 @@ scene script and seed.  Bars as test_parity_gpu.check."""
 import numpy as np
 import pytest
 
+import objimg
 from conftest import rmse_per_channel
 from test_parity_gpu import check, render_both
 
@@ -232,3 +233,36 @@ def test_image_texture(gpu, oracle, rt, linear):
     out, st = render_both(gpu, oracle, rt, build)
     check(out)
     assert st["gpu"].panics == 0
+
+
+@pytest.mark.parametrize("names", [["tile", "glass", "bumpy"], ["lamp", "leaf", "lampleaf"]])
+def test_obj_image_materials(gpu, oracle, rt, capi, tmp_path, names):
+    """map_Kd -> ImageTexture (a vanilla Metal takes its pixel at (0, 0), a
+    Dielectric the texture), map_Ke -> DiffuseLight(image, mat), map_d ->
+    Mix::from_image(Transparent, mat) (the alpha as the ratio), map_Bump ->
+    a raw bilinear normal map; PNGs decoded by the library (rt_png.hpp).  The
+    second case nests wrappers (Mix of DiffuseLight(image, DiffuseLight(Ke,
+    Metal))) -- the FULL_GL tier."""
+    pytest.importorskip("PIL")
+    objimg.write_scene(tmp_path, names)
+
+    def build(s):
+        world = s.Hittables()
+        world.add(s.Wavefont(str(tmp_path / "scene.obj")))
+        world.add(s.Sphere((0, -100.2, 0), 100, s.Lambertian(s.SolidColor((0.4, 0.45, 0.4)))))
+        cam = rt.Camera()
+        cam.aspect_ratio = 16 / 9
+        cam.image_width = 96
+        cam.samples_per_pixel = 16
+        cam.max_depth = 12
+        cam.vertical_fov_in_degrees = 50.0
+        cam.look_from = (0.0, 1.2, 4.0)
+        cam.look_at = (-0.4, 0.6, 0.0)
+        cam.background = s.SkyGradient((1.0, 1.0, 1.0), (0.5, 0.7, 1.0))
+        return world, None, cam
+    out, st = render_both(gpu, oracle, rt, build)
+    check(out)
+    assert st["gpu"].panics == st["oracle"].panics == 0
+    s = rt.Scene(gpu)
+    w, l, c = build(s)
+    assert _tier(gpu, capi, s, w, l, c) == (4 if "leaf" in names else 2)

@@ -277,3 +277,37 @@ def _wrap(s, path):
     w = s.Hittables()
     w.add(s.Wavefont(path))
     return w
+
+
+@pytest.mark.parametrize("names,tier", [(["tile", "glass", "bumpy"], 2), (["lamp", "leaf", "lampleaf"], 4)])
+def test_obj_image_maps_load(product, oracle, rt, capi, tmp_path, names, tier):
+    """map_Kd / map_Ke / map_d / map_Bump images decode (rt_png.hpp) and load
+    in both implementations; wrapper nesting and Mix::from_image select the
+    FULL_GL tier; a vanilla Metal over map_Kd takes the pixel at (0, 0)."""
+    pytest.importorskip("PIL")
+    import ctypes
+    import objimg
+    p = objimg.write_scene(tmp_path, names)
+    for api in (product, oracle):
+        s = rt.Scene(api)
+        w = s.Hittables()
+        w.add(s.Wavefont(p))
+    s = rt.Scene(product)
+    w = s.Wavefont(p)
+    info = capi.RtWorldInfo()
+    product.check(product.world_info_get(s.s, w.h, -1, -1, 0, ctypes.byref(info)))
+    assert info.kernel_tier == tier and info.primitives == 2 * len(names)
+
+
+def test_reference_mc_obj_needs_disney(product, oracle, rt, capi):
+    """The reference's own assets/Final/mc.obj (read in place) decodes its PNG
+    maps (4-bit palette, gray, RGBA) but its materials are Disney BSDFs
+    (no Pm / Tf, obj.rs:299-311): out of scope, RT_EUNSUPPORTED in both."""
+    path = "/root/reference/assets/Final/mc.obj"
+    if not os.path.exists(path):
+        pytest.skip("reference assets not mounted")
+    for api in (product, oracle):
+        s = rt.Scene(api)
+        with pytest.raises(capi.RtError) as e:
+            s.Wavefont(path)
+        assert e.value.code == -6 and b"Disney" in api.last_error()

@@ -1,0 +1,107 @@
+"""ImageTexture's PNG decoding (raytracer-2025_amd/csrc/rt_png.hpp, shared by
+the library's loaders and the oracle) against PIL: the `image` crate's
+into_rgba32f (8-bit v / 255, 16-bit v / 65535, gray -> (g, g, g), palette +
+tRNS -> RGBA) on the reference's own PNG assets read in place (4-bit palette,
+8-bit gray, RGB, RGBA) and on synthetic files of every color type / bit depth
+PIL writes; then palette's sRGB EOTF in f32 (utils/image.rs:63-82) against
+the formula in numpy.  A missing file is Image::EMPTY; JPEG and interlaced
+PNG are reported unsupported (never read as something else)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+REF_ASSETS = "/root/reference/assets/Final"
+
+PIL = pytest.importorskip("PIL.Image")
+
+
+@pytest.fixture(scope="module")
+def dump():
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, "png_dump")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", os.path.join(HERE, "cpp", "png_dump.cpp"), "-o",
+                    exe, "-lz"], check=True)
+
+    def run(path, raw, tmp):
+        out = os.path.join(str(tmp), "dump.bin")
+        r = subprocess.run([exe, path, out, "1" if raw else "0"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        with open(out, "rb") as f:
+            st, w, h = map(int, f.readline().split())
+            px = np.frombuffer(f.read(), dtype=np.float32)
+        return st, px.reshape(h, w, 4) if st == 0 else None
+    return run
+
+
+def pil_rgba01(path):
+    im = PIL.open(path)
+    if im.mode in ("I;16", "I;16B", "I"):
+        a = np.asarray(im, dtype=np.float32) / 65535.0
+        return np.stack([a, a, a, np.ones_like(a)], axis=-1)
+    return np.asarray(im.convert("RGBA"), dtype=np.float32) / 255.0
+
+
+def srgb_to_linear(x):
+    x = x.astype(np.float32)
+    return np.where(x <= np.float32(0.04045), x / np.float32(12.92),
+                    np.power((x + np.float32(0.055)) / np.float32(1.055), np.float32(2.4))).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["diamond_ore.png", "diamond_pickaxe.png", "stone.png", "torch.png", "flame.png",
+                                  "门_框_Metallic.png"])
+def test_reference_assets_match_pil(dump, tmp_path, name):
+    path = os.path.join(REF_ASSETS, name)
+    if not os.path.exists(path):
+        pytest.skip("reference assets not mounted")
+    st, px = dump(path, True, tmp_path)
+    assert st == 0
+    ref = pil_rgba01(path)
+    assert px.shape == ref.shape
+    np.testing.assert_array_equal(px, ref)
+    st, lin = dump(path, False, tmp_path)
+    np.testing.assert_allclose(lin[..., :3], srgb_to_linear(ref[..., :3]), rtol=2e-6, atol=1e-7)
+    np.testing.assert_array_equal(lin[..., 3], ref[..., 3])
+
+
+@pytest.mark.parametrize("mode", ["L", "LA", "RGB", "RGBA", "P", "P_trns", "1", "I;16"])
+def test_synthetic_modes_match_pil(dump, tmp_path, mode):
+    rng = np.random.default_rng(len(mode))
+    h, w = 23, 37  # odd sizes: sub-byte rows, every filter type PIL picks
+    if mode in ("L", "LA", "RGB", "RGBA"):
+        ch = {"L": 1, "LA": 2, "RGB": 3, "RGBA": 4}[mode]
+        a = rng.integers(0, 256, size=(h, w, ch), dtype=np.uint8)
+        a[: h // 2] = (np.arange(w)[None, :, None] * 7 % 256).astype(np.uint8)  # smooth half: Sub/Up/Paeth rows
+        im = PIL.fromarray(a[..., 0] if ch == 1 else a, mode)
+    elif mode.startswith("P"):
+        im = PIL.fromarray(rng.integers(0, 200, size=(h, w, 3), dtype=np.uint8), "RGB").quantize(colors=13)
+        if mode == "P_trns":
+            im.info["transparency"] = 3
+    elif mode == "1":
+        im = PIL.fromarray((rng.random((h, w)) > 0.5).astype(np.uint8) * 255, "L").convert("1")
+    else:
+        im = PIL.fromarray(rng.integers(0, 65536, size=(h, w), dtype=np.uint16))  # mode I;16
+    path = str(tmp_path / f"m_{mode.replace(';', '')}.png")
+    kw = {"transparency": 3} if mode == "P_trns" else {}
+    im.save(path, **kw)
+    st, px = dump(path, True, tmp_path)
+    assert st == 0
+    ref = pil_rgba01(path)
+    np.testing.assert_array_equal(px, ref)
+
+
+def test_missing_and_unsupported(dump, tmp_path):
+    st, _ = dump(str(tmp_path / "absent.png"), False, tmp_path)
+    assert st == 1  # Image::EMPTY -> cyan
+    (tmp_path / "broken.png").write_bytes(b"\x89PNG\r\n\x1a\n" + b"\x00" * 40)
+    assert dump(str(tmp_path / "broken.png"), False, tmp_path)[0] == 1  # decode error -> EMPTY, as the reference
+    PIL.new("RGB", (8, 8)).save(str(tmp_path / "x.jpg"))
+    assert dump(str(tmp_path / "x.jpg"), False, tmp_path)[0] == 3
+    PIL.new("RGB", (9, 9), (10, 20, 30)).save(str(tmp_path / "il.png"), interlace=1)
+    st, px = dump(str(tmp_path / "il.png"), False, tmp_path)
+    assert st in (0, 3)  # PIL may not interlace; an interlaced file is reported, never misread
+    if st == 0:
+        np.testing.assert_array_equal(px[..., :3], srgb_to_linear(pil_rgba01(str(tmp_path / "il.png"))[..., :3]))
