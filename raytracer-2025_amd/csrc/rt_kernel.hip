@@ -598,21 +598,89 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // ConstantMedium::hit (volume.rs:37-73) of medium idx for ray r in the
 // medium's frame, interval [tmin, tmax]: the two boundary hits are one
 // boundary walk run twice (one copy of the walk in the code).
+#ifndef RT_MED_ONEPASS
+#define RT_MED_ONEPASS 1
+#endif
+// The two boundary hits of a boundary made of one sphere or of planar_n
+// consecutive quads / triangles (rt_scene.cpp planar_boundary) in one pass.  A
+// planar test's t and inside decision do not depend on the interval (quad.rs:
+// 71-102: the interval only accepts or rejects the t already computed), so
+// each element is tested once over (-inf, inf) and its t kept; the first hit
+// is the least t (Hittables::hit, hits.rs:34-46), the second the least t >=
+// t1 + 0.0001 -- the values and decisions of the two walks of volume.rs:44-48,
+// without the list walk and with one planar test per element instead of two.
+__device__ __forceinline__ bool boundary_onepass(const SceneView& S, const DMedium& M, const Ray& r0, double& t1,
+                                                double& t2) {
+    const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
+    Ray r = r0;  // into the frame of the Transforms around the elements, as the walk does
+    for (uint32_t j = 0; j < M.bxf_n; ++j) r = xf_ray(S.xforms[j == 0 ? M.bxf[0] : M.bxf[1]], r);
+    if (M.bsphere) {
+        // sphere.rs:77-92 over (-inf, inf), then over [t1 + 0.0001, inf):
+        // the same roots, chosen by each interval as sphere_t_inv chooses
+        const double4 s4 = S.spheres[M.bsphere - 1];
+        const double a = len2(r.d), inva = 1.0 / a;
+        const D3 oc = d3(s4.x, s4.y, s4.z) - r.o;
+        const double h = dot(r.d, oc);
+        const double cc = len2(oc) - s4.w * s4.w;
+        const double disc = h * h - a * cc;
+        if (disc < 0.0) return false;
+        const double sq = sqrt(disc);
+        const double rn = div_a(h - sq, a, inva), rf = div_a(h + sq, a, inva);
+        auto pick = [&](double lo, double& t) {
+            if (rn >= lo && rn <= PINF) t = rn;
+            else if (rf >= lo && rf <= PINF) t = rf;
+            else return false;
+            return true;
+        };
+        if (!pick(NINF, t1)) return false;
+        return pick(fmin(t1 + 0.0001, PINF), t2);
+    }
+    double tv[RT_MED_PLANAR_MAX];
+    bool any = false;
+    t1 = PINF;
+#pragma unroll
+    for (uint32_t k = 0; k < RT_MED_PLANAR_MAX; ++k) {
+        tv[k] = __builtin_nan("");
+        double tt;
+        if (k < M.planar_n && planar_t(S.planars[M.planar_first + k], (M.tri_mask >> k) & 1u, r, NINF, PINF, tt)) {
+            tv[k] = tt;
+            t1 = any ? fmin(t1, tt) : tt;
+            any = true;
+        }
+    }
+    if (!any) return false;
+    const double lo = fmin(t1 + 0.0001, PINF);
+    any = false;
+    t2 = PINF;
+#pragma unroll
+    for (uint32_t k = 0; k < RT_MED_PLANAR_MAX; ++k) {
+        if (tv[k] >= lo && tv[k] <= PINF) {  // NaN (no hit) fails both
+            t2 = any ? fmin(t2, tv[k]) : tv[k];
+            any = true;
+        }
+    }
+    return any;
+}
+
 template <bool BVH, class Stack>
 __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, const Ray& r, double tmin, double tmax,
                                            Stack& stk, uint32_t sp0, const Rng& rng, double& t) {
     const DMedium M = S.media[idx];
     const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
     double t1 = 0.0, t2 = 0.0, lo = NINF;
+    if (RT_MED_ONEPASS && (M.planar_n || M.bsphere)) {
+        if (!boundary_onepass(S, M, r, t1, t2)) return false;
+    } else {
 #pragma nounroll
-    for (int pass = 0; pass < 2; ++pass) {
-        double tb;
-        if (!boundary_t<BVH>(S, M.boundary, r, lo, PINF, stk, sp0, tb)) return false;
-        if (pass == 0) {
-            t1 = tb;
-            lo = fmin(t1 + 0.0001, PINF);
-        } else {
-            t2 = tb;
+        for (int pass = 0; pass < 2; ++pass) {
+            double tb;
+            if (!boundary_t<BVH>(S, M.boundary, r, lo, PINF, stk, sp0, tb)) return false;
+            if (pass == 0) {
+                t1 = tb;
+                lo = fmin(t1 + 0.0001, PINF);
+            } else {
+                t2 = tb;
+            }
         }
     }
     if (t1 < tmin) t1 = tmin;

@@ -129,12 +129,24 @@ struct alignas(16) DXform {
     uint32_t child, pad;
 };
 
+constexpr uint32_t RT_MED_PLANAR_MAX = 6;  // elements of a one-pass medium boundary (build_box: 6)
+
 // ConstantMedium (volume.rs:16-20)
 struct alignas(16) DMedium {
     double neg_inv_density;
     uint32_t boundary;
     int32_t phase_mat;
     uint32_t medium_id;
+    // > 0: the boundary is planar_n quads / triangles stored consecutively at
+    // planars[planar_first ..] (build_box's six quads), inside at most two
+    // Transforms, tested in one pass (rt_kernel.hip medium_hit); 0: any other
+    // boundary, walked twice
+    uint32_t planar_n;
+    uint32_t planar_first;
+    uint32_t tri_mask;  // bit k: element k is a triangle
+    uint32_t bxf_n;     // Transforms around those elements (outermost first)
+    uint32_t bxf[2];
+    uint32_t bsphere;   // > 0: the boundary is spheres[bsphere - 1] (inside bxf), one pass too
     uint32_t pad;
 };
 

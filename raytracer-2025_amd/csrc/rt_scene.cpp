@@ -353,6 +353,44 @@ struct Flattener {
         }
     }
 
+    // A medium boundary that is one sphere, one quad / triangle or a flat list
+    // of at most RT_MED_PLANAR_MAX of them stored consecutively (build_box),
+    // inside at most two Transforms, is marked for the kernel's one-pass
+    // boundary test; anything else keeps planar_n = bsphere = 0.
+    void planar_boundary(uint32_t ref, rtk::DMedium& m) const {
+        auto planar = [](uint32_t r) { return rtk::ref_kind(r) == rtk::K_QUAD || rtk::ref_kind(r) == rtk::K_TRI; };
+        m.planar_n = m.planar_first = m.tri_mask = m.bxf_n = m.bsphere = 0;
+        m.bxf[0] = m.bxf[1] = 0;
+        uint32_t nxf = 0;
+        while (rtk::ref_kind(ref) == rtk::K_XFORM) {
+            if (nxf == 2) return;
+            m.bxf[nxf++] = rtk::ref_index(ref);
+            ref = out.xforms[rtk::ref_index(ref)].child;
+        }
+        if (rtk::ref_kind(ref) == rtk::K_SPHERE) {
+            m.bsphere = rtk::ref_index(ref) + 1;
+            m.bxf_n = nxf;
+            return;
+        }
+        std::vector<uint32_t> el;
+        if (planar(ref)) {
+            el.push_back(ref);
+        } else if (rtk::ref_kind(ref) == rtk::K_LIST) {
+            for (uint32_t li = rtk::ref_index(ref); out.list_children[li] != REF_NONE_; ++li) {
+                if (!planar(out.list_children[li]) || el.size() >= rtk::RT_MED_PLANAR_MAX) return;
+                el.push_back(out.list_children[li]);
+            }
+        }
+        if (el.empty()) return;
+        for (size_t k = 0; k < el.size(); ++k) {
+            if (rtk::ref_index(el[k]) != rtk::ref_index(el[0]) + k) return;
+            if (rtk::ref_kind(el[k]) == rtk::K_TRI) m.tri_mask |= 1u << k;
+        }
+        m.planar_first = rtk::ref_index(el[0]);
+        m.planar_n = (uint32_t)el.size();
+        m.bxf_n = nxf;
+    }
+
     // Returns (ref, need): need = traversal-stack entries used below the entry
     // that held this ref (rt_kernel.hip trace()).
     std::pair<uint32_t, uint32_t> emit(int id, bool in_boundary, int xf_depth) {
@@ -528,6 +566,7 @@ struct Flattener {
                 m.boundary = B.first;
                 m.phase_mat = o.phase_mat;
                 m.medium_id = o.medium_id;
+                planar_boundary(B.first, m);
                 out.media.push_back(m);
                 out.features |= rtk::F_MEDIUM;
                 r = {rtk::make_ref(rtk::K_MEDIUM, idx), B.second};

@@ -10,7 +10,7 @@ mkdir -p $OUT
 { nproc; cat /sys/fs/cgroup/cpu.max 2>&1; python3 -c "import os;print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count())"; lscpu | head -20; } > $OUT/host.txt 2>&1
 fatal() { case $1 in 0|1) return 1;; *) echo "fatal rc=$1 in $2"; return 0;; esac; }
 if [ "${R02_TESTS:-1}" = 1 ]; then
-  timeout -k 10 ${R02_TEST_TIMEOUT:-800} python3 -u -m pytest tests -m gpu -v -s ${R02_TEST_ARGS:-} --timeout 400 --timeout-method thread > $OUT/pytest.log 2>&1
+  timeout -k 10 ${R02_TEST_TIMEOUT:-800} python3 -u -m pytest tests -m gpu -v -s ${R02_TEST_ARGS:-} ${R02_K:+-k "$R02_K"} --timeout 400 --timeout-method thread > $OUT/pytest.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -40 $OUT/pytest.log | grep -E "passed|failed|FAILED|Error" | tail -30
   if fatal $rc pytest; then exit 1; fi
 fi

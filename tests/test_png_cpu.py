@@ -22,7 +22,7 @@ PIL = pytest.importorskip("PIL.Image")
 @pytest.fixture(scope="module")
 def dump():
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "png_dump")
+    exe = os.path.join(BUILD, "png_dump.%d" % os.getpid())  # one per pytest worker
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", os.path.join(HERE, "cpp", "png_dump.cpp"), "-o",
                     exe, "-lz"], check=True)
 
