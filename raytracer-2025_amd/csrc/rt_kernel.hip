@@ -467,6 +467,11 @@ constexpr float NO_CULL = -__builtin_huge_valf();
 #endif
 template <int TIER>
 constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXES; }
+#ifndef RT_FLAT_RUNS
+#define RT_FLAT_RUNS 1  // the flat tier's list step tests a whole planar run (DBoxF::run)
+#endif
+template <int TIER>
+constexpr bool flat_runs() { return TIER == TIER_FULL_FLAT && RT_FLAT_RUNS; }
 #ifndef RT_FLAT_BOUNDARY_BOXES
 #define RT_FLAT_BOUNDARY_BOXES 0  // the medium boundary walks test element boxes too
 #endif
@@ -761,6 +766,15 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     const Ray& r = FULL ? T.r : wr;
     uint32_t cur = T.cur;
     T.cur = REF_NONE;
+    auto record = [&](uint32_t ref, double tt) {
+        T.found = true;
+        T.hit.t = tt;
+        T.hit.ref = ref;
+        if constexpr (FULL) {
+            T.hit.nxf = T.nxf;
+            T.hit.xf = T.xfs;
+        }
+    };
     // A list step whose element is a primitive tests it right here and goes
     // on with the next element (no stack round trip, one step per element);
     // a compound element (BVH, Transform, medium, list) is walked next with
@@ -770,6 +784,26 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         const uint32_t li = ref_index(cur);
         const uint32_t child = S.list_children[li];
         if (child == REF_NONE) return true;  // empty list
+        if constexpr (flat_runs<TIER>()) {
+            // the flat tier tests a run of planar elements (the Cornell walls,
+            // a box's six faces) in one step, in list order, each against the
+            // closest t so far -- what the run's single steps do
+            const uint32_t ck0 = ref_kind(child);
+            if (ck0 == K_QUAD || ck0 == K_TRI) {
+                const uint32_t run = S.list_boxes[li].run, n = run & 0xffu, first = ref_index(child);
+                RT_DIAG_ONLY(++dg.lane_trace_iters; dg.sphere_tests += n;)
+                for (uint32_t k = 0; k < n; ++k) {
+                    const bool tri = (run >> (8u + k)) & 1u;
+                    double tt;
+                    if (planar_t_filtered(S, first + k, tri, r, tmin, T.cl.c, T.cl.c_f, tt)) {
+                        T.cl.set(tt);
+                        record(make_ref(tri ? K_TRI : K_QUAD, first + k), tt);
+                    }
+                }
+                T.cur = S.list_children[li + n] != REF_NONE ? make_ref(K_LIST, li + n) : REF_NONE;
+                return true;
+            }
+        }
         const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
         if constexpr (flat_boxes<TIER>()) {
             const uint32_t ck = ref_kind(child);
@@ -793,15 +827,6 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     const uint32_t this_ref = cur;
     double t;
     bool got = false;
-    auto record = [&](uint32_t ref, double tt) {
-        T.found = true;
-        T.hit.t = tt;
-        T.hit.ref = ref;
-        if constexpr (FULL) {
-            T.hit.nxf = T.nxf;
-            T.hit.xf = T.xfs;
-        }
-    };
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
     if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
         if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4))

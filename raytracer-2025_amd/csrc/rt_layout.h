@@ -90,10 +90,14 @@ struct alignas(16) DNode4 {
 static_assert(sizeof(DNode4) == 112, "DNode4 must be 112 B (7 dwordx4)");
 
 // f32 box of one list element (list_boxes, parallel to list_children),
-// rounded outward: the flat tier tests it before the element itself.
+// rounded outward: the flat tier tests it before the element itself.  run:
+// for a quad / triangle element, the number n (<= RT_PLANAR_RUN_MAX) of
+// planar elements from this one on whose planar indices follow each other,
+// with bit 8 + k set when element k of the run is a triangle (0 otherwise).
+constexpr uint32_t RT_PLANAR_RUN_MAX = 8;
 struct alignas(16) DBoxF {
     float lo[3], hi[3];
-    uint32_t pad[2];
+    uint32_t run, pad;
 };
 static_assert(sizeof(DBoxF) == 32, "DBoxF must be 32 B (2 dwordx4)");
 

@@ -789,6 +789,23 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         out.list_children.push_back(rtk::REF_NONE);
         out.list_boxes.push_back(rtk::DBoxF{});
     }
+    // planar runs of the lists (DBoxF::run): the flat tier tests a run in one
+    // walk step
+    auto planar = [](uint32_t r) { return rtk::ref_kind(r) == rtk::K_QUAD || rtk::ref_kind(r) == rtk::K_TRI; };
+    for (size_t i = 0; i < out.list_children.size(); ++i) {
+        const uint32_t c = out.list_children[i];
+        uint32_t run = 0;
+        if (planar(c)) {
+            uint32_t n = 0;
+            while (n < rtk::RT_PLANAR_RUN_MAX && i + n < out.list_children.size() && planar(out.list_children[i + n]) &&
+                   rtk::ref_index(out.list_children[i + n]) == rtk::ref_index(c) + n) {
+                if (rtk::ref_kind(out.list_children[i + n]) == rtk::K_TRI) run |= 1u << (8 + n);
+                ++n;
+            }
+            run |= n;
+        }
+        out.list_boxes[i].run = run;
+    }
     return RT_OK;
 }
 
