@@ -261,13 +261,13 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
 // branches.  Kept as an option.
 #define RT_PLANAR_EARLY 0
 #endif
-// quad.rs:71-102 / triangle.rs:69-98
-__device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& r, double tmin, double tmax,
-                                         double& t) {
-    const D3 n = d3(P.f[0], P.f[1], P.f[2]);
+// quad.rs:71-102 / triangle.rs:69-98 on the record's values: unit normal n,
+// parm_d D, anchor Q, edges u / v, w = n / |n|^2
+__device__ __forceinline__ bool planar_t_v(const D3 n, const double D, const D3 Q, const D3 u, const D3 v, const D3 w,
+                                           bool tri, const Ray& r, double tmin, double tmax, double& t) {
     const double denom = dot(n, r.d);
     if (fabs(denom) < 1e-8) return false;
-    const double num = P.f[3] - dot(n, r.o);
+    const double num = D - dot(n, r.o);
     if constexpr (RT_PLANAR_EARLY) {
         const bool same = (num < 0.0) == (denom < 0.0);
         if (!same && num != 0.0 && tmin >= 0.0) return false;
@@ -275,8 +275,7 @@ __device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& 
     }
     const double tt = num / denom;
     if (!(tt >= tmin && tt <= tmax)) return false;
-    const D3 hv = (r.o + tt * r.d) - d3(P.f[4], P.f[5], P.f[6]);
-    const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
+    const D3 hv = (r.o + tt * r.d) - Q;
     const double alpha = dot(w, cross(hv, v));
     if (RT_PLANAR_EARLY && !(alpha >= 0.0 && alpha <= 1.0)) return false;
     const double beta = dot(w, cross(u, hv));
@@ -287,6 +286,12 @@ __device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& 
     }
     t = tt;
     return true;
+}
+// quad.rs:71-102 / triangle.rs:69-98
+__device__ __forceinline__ bool planar_t(const DPlanar& P, bool tri, const Ray& r, double tmin, double tmax,
+                                         double& t) {
+    return planar_t_v(d3(P.f[0], P.f[1], P.f[2]), P.f[3], d3(P.f[4], P.f[5], P.f[6]), d3(P.f[7], P.f[8], P.f[9]),
+                      d3(P.f[10], P.f[11], P.f[12]), d3(P.f[13], P.f[14], P.f[15]), tri, r, tmin, tmax, t);
 }
 
 #ifndef RT_PLANAR_FILTER
@@ -467,6 +472,16 @@ constexpr float NO_CULL = -__builtin_huge_valf();
 #endif
 template <int TIER>
 constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXES; }
+#ifndef RT_UNIFIED_LOAD
+#define RT_UNIFIED_LOAD 1  // mesh / full tiers: one load per walk step for node / planar / sphere records
+#endif
+template <int TIER>
+constexpr bool unified_load() {
+    return ((TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4)) && RT_UNIFIED_LOAD;
+}
+// the two doubles of a float4 read from a double record
+__device__ __forceinline__ double f4_lo(float4 q) { return __hiloint2double(__float_as_int(q.y), __float_as_int(q.x)); }
+__device__ __forceinline__ double f4_hi(float4 q) { return __hiloint2double(__float_as_int(q.w), __float_as_int(q.z)); }
 #ifndef RT_FLAT_RUNS
 #define RT_FLAT_RUNS 1  // the flat tier's list step tests a whole planar run (DBoxF::run)
 #endif
@@ -828,6 +843,40 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
     double t;
     bool got = false;
     RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
+    if (unified_load<TIER>() && (kind == K_BVH || kind == K_SPHERE || kind == K_TRI || kind == K_QUAD)) {
+        // One load for the step's record, whatever it is: a node's 7 rows, a
+        // quad's / triangle's 128 B, a sphere's 32 B, read as 8 dwordx4 from
+        // the record's address (the world blob is padded past every array).
+        // In a wave whose lanes hold nodes and primitives both, the node
+        // visit and the primitive test then wait on one memory latency, not
+        // one after the other.
+        const bool planar = kind == K_TRI || kind == K_QUAD;
+        // (the array addresses as values, selected: a select between the
+        // SceneView's members made the compiler index a scratch copy of it)
+        const uint64_t a_node = (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars, a_sphere = (uint64_t)S.spheres;
+        uint64_t addr = a_node;
+        uint32_t stride = 0u;
+        if (kind == K_BVH) stride = (uint32_t)sizeof(DNode4);
+        if (planar) addr = a_planar, stride = (uint32_t)sizeof(DPlanar);
+        if (kind == K_SPHERE) addr = a_sphere, stride = (uint32_t)sizeof(double4);
+        const RT_GLOBAL float4* q = reinterpret_cast<const RT_GLOBAL float4*>(addr + (uint64_t)idx * stride);
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6], q7 = q[7];
+        if (kind == K_BVH) {
+            T.cur = visit4_boxes_rows(q0, q1, q2, q3, q4, q5, q6, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
+        } else if (kind == K_SPHERE) {
+            got = sphere_t_inv(d3(f4_lo(q0), f4_hi(q0), f4_lo(q1)), f4_hi(q1), r, T.a, T.inva, tmin, T.cl.c, t);
+        } else if (planar) {
+            got = planar_t_v(d3(f4_lo(q0), f4_hi(q0), f4_lo(q1)), f4_hi(q1), d3(f4_lo(q2), f4_hi(q2), f4_lo(q3)),
+                             d3(f4_hi(q3), f4_lo(q4), f4_hi(q4)), d3(f4_lo(q5), f4_hi(q5), f4_lo(q6)),
+                             d3(f4_hi(q6), f4_lo(q7), f4_hi(q7)), kind == K_TRI, r, tmin, T.cl.c, t);
+        }
+        if (got) {
+            T.cl.set(t);
+            record(this_ref, t);
+        }
+        if (after != REF_NONE) T.cur = after;
+        return true;
+    }
     if (TIER != TIER_FULL_FLAT && kind == K_BVH) {
         if constexpr ((TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4))
             T.cur = visit4_boxes(S, idx, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
@@ -995,10 +1044,21 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
 // and the others pushed farthest first -- primitives included, so a triangle
 // is tested (planar_t) when the walk reaches it, in distance order.
 template <class Stack>
+__device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const float4 ly, const float4 lz,
+                                                      const float4 hx, const float4 hy, const float4 hz,
+                                                      const float4 rq, const RayF& rf, float tmin_f, float c_f,
+                                                      Stack& stk, uint32_t& sp);
+template <class Stack>
 __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
                                                  float c_f, Stack& stk, uint32_t& sp) {
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
-    const float4 lx = np[0], ly = np[1], lz = np[2], hx = np[3], hy = np[4], hz = np[5], rq = np[6];
+    return visit4_boxes_rows(np[0], np[1], np[2], np[3], np[4], np[5], np[6], rf, tmin_f, c_f, stk, sp);
+}
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const float4 ly, const float4 lz,
+                                                      const float4 hx, const float4 hy, const float4 hz,
+                                                      const float4 rq, const RayF& rf, float tmin_f, float c_f,
+                                                      Stack& stk, uint32_t& sp) {
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};

@@ -305,6 +305,9 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.textures = (const rtk::DTexture*)off(put(blob, hw.textures));
     v.texels = (const float*)off(put(blob, hw.texels));
     v.perlin = (const rtk::DPerlin*)off(put(blob, hw.perlin));
+    // the mesh tier reads 128 B from any record's address (rt_kernel.hip
+    // unified_load): slack past the last array
+    blob.resize(((blob.size() + 255) & ~(size_t)255) + 256, 0);
     v.world_root = hw.world_root;
     v.lights_root = hw.lights_root;
     v.background_tex = bg;
