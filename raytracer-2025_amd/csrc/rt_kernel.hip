@@ -1442,6 +1442,17 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
     return light_random_one(S, ref, o, rng, ovf, ok);
 }
 
+#ifndef RT_SOLID_ALBEDO
+#define RT_SOLID_ALBEDO 1
+#endif
+// A material's texture value; a SolidColor's colour comes with the material
+// record (MF_SOLID, set by the flatten), one dependent load fewer.
+template <bool FULL>
+__device__ __forceinline__ D3 mat_tex(const SceneView& S, const DMaterial& M, double u, double v, D3 p) {
+    if (RT_SOLID_ALBEDO && (M.flags & MF_SOLID)) return d3(M.albedo[0], M.albedo[1], M.albedo[2]);
+    return tex_value<FULL>(S, M.tex, u, v, p);
+}
+
 // vec3.rs:313-322
 __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
@@ -1469,7 +1480,7 @@ template <int D>
 __device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p) {
     const DMaterial& M = S.materials[mid];
     if (M.type == M_DIFFUSE_LIGHT) {
-        const D3 self = tex_value<true>(S, M.tex, u, v, p);
+        const D3 self = mat_tex<true>(S, M, u, v, p);
         D3 inner = d3(0.0, 0.0, 0.0);
         if constexpr (D > 0)
             if (M.inner >= 0) inner = emitted_tree<D - 1>(S, M.inner, u, v, p);
@@ -1540,12 +1551,12 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
         if (M.flags & MF_EMISSIVE) {
             D3 em;
             if (M.type == M_DIFFUSE_LIGHT) {
-                em = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+                em = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
             } else {  // Mix of non-wrapping materials (flatten checks)
                 const DMaterial& A = S.materials[M.inner];
                 const DMaterial& B = S.materials[M.inner2];
-                const D3 ea = A.type == M_DIFFUSE_LIGHT ? tex_value<FULL>(S, A.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
-                const D3 eb = B.type == M_DIFFUSE_LIGHT ? tex_value<FULL>(S, B.tex, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                const D3 ea = A.type == M_DIFFUSE_LIGHT ? mat_tex<FULL>(S, A, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                const D3 eb = B.type == M_DIFFUSE_LIGHT ? mat_tex<FULL>(S, B, rec.u, rec.v, rec.p) : d3(0, 0, 0);
                 em = ((1.0 - M.fuzz) * ea) + (M.fuzz * eb);
             }
             L = L + beta * em;
@@ -1565,7 +1576,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     D3 albedo = d3(0, 0, 0);
     switch (M.type) {
         case M_LAMBERTIAN:  // material.rs:60-65
-            albedo = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+            albedo = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
             pdf_kind = 0;
             break;
         case M_EMPTY:  // material.rs:41-46
@@ -1613,14 +1624,14 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 if (isnan(pl)) panic = true;
                 dir = perp + (-pl * n);
             }
-            beta = beta * tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+            beta = beta * mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
             ray = Ray{rec.p, dir, ray.time};
             break;
         }
         default:
             if constexpr (FULL) {
                 if (M.type == M_ISOTROPIC) {  // material.rs:199-206
-                    albedo = tex_value<FULL>(S, M.tex, rec.u, rec.v, rec.p);
+                    albedo = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
                     pdf_kind = 1;
                     break;
                 }

@@ -171,12 +171,13 @@ struct alignas(16) DMaterial {
     int32_t tex;       // albedo / attenuation / emission texture
     int32_t inner;     // DiffuseLight inner material, Mix mat1
     int32_t inner2;    // Mix mat2
-    double albedo[3];  // Metal albedo
+    double albedo[3];  // Metal albedo; the solid texture's colour (MF_SOLID)
     double fuzz;       // Metal fuzz (clamped), Dielectric ior, Mix ratio
     uint32_t flags;    // MF_*
     uint32_t pad[3];
 };
-enum : uint32_t { MF_NEEDS_UV = 1u, MF_EMISSIVE = 2u };
+// MF_SOLID: tex is a SolidColor, whose colour albedo holds (not for Metal)
+enum : uint32_t { MF_NEEDS_UV = 1u, MF_EMISSIVE = 2u, MF_SOLID = 4u };
 
 enum TexType : int32_t {
     T_SOLID = 0,

@@ -677,6 +677,12 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
         uint32_t f = 0;
         if (m.tex >= 0 && tex_needs_uv(s, m.tex)) f |= rtk::MF_NEEDS_UV;
         if (m.type == rtk::M_DIFFUSE_LIGHT) f |= rtk::MF_EMISSIVE;
+        // a solid-colour texture on a material that does not use albedo
+        // itself: the colour in albedo, read with the material record
+        if (m.type != rtk::M_METAL && m.tex >= 0 && s->texs[m.tex].type == rtk::T_SOLID) {
+            f |= rtk::MF_SOLID;
+            for (int k = 0; k < 3; ++k) m.albedo[k] = s->texs[m.tex].color[k];
+        }
         m.flags = f;
     }
     for (int pass = 0; pass < 4; ++pass)
