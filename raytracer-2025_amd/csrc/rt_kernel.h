@@ -9,17 +9,19 @@
 #define RT_BLOCK 256        // 4 waves of 64 (mesh and full tiers)
 // Basic tier: one 1024-thread block per CU (16 waves, 4 per SIMD: the same
 // 128-VGPR budget) so that one LDS copy of the world's 4-wide nodes serves
-// the whole CU.  LDS: stack entries * 1024 * 8 B + the sphere queue
-// (RT_PEND_CAP * 1024 * 2 B) + RT_NODE_LDS_BYTES of nodes <= 160 KiB.
+// the whole CU.  LDS: stack entries * 1024 * 4 B (RT_STACK4B) + the sphere
+// queue (RT_PEND_CAP * 1024 * 2 B) + RT_NODE_LDS_BYTES of nodes <= 160 KiB.
 #ifndef RT_BLOCK_BASIC
 #define RT_BLOCK_BASIC 1024
 #endif
-// traversal-stack entries per lane; LDS = entries * block * 8 B
+// traversal-stack entries per lane; LDS = entries * block * 4 B
 #ifndef RT_STACK_BASIC
-#define RT_STACK_BASIC 14   // 112 KiB of the basic tier's 1024-lane block
+#define RT_STACK_BASIC 14   // 56 KiB of the basic tier's 1024-lane block
 #endif
 #ifndef RT_NODE_LDS_BYTES
-#define RT_NODE_LDS_BYTES 32704  // basic tier: the first 292 DNode4 of the world in LDS
+// basic tier: the world's 4-wide nodes in LDS, 804 of them (about 1 600
+// spheres): 160 KiB - 56 KiB of stack - 16 KiB of sphere queue, in 112-B nodes
+#define RT_NODE_LDS_BYTES 90048
 #endif
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)

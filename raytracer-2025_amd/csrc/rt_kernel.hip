@@ -357,6 +357,9 @@ struct HitInfo {
 // per half-wave.  With OVF, entries k >= CAP (deep triangle BVHs) live in the
 // lane's column of a global overflow buffer, [k - CAP][lane of the grid], so
 // the LDS part stays small enough for 4 blocks per CU.
+#ifndef RT_STACK4B
+#define RT_STACK4B 1
+#endif
 template <uint32_t CAP, bool OVF, uint32_t BLK>
 struct StackT {
     RT_LDS uint2* base;  // explicitly LDS: a select against ovf must not become a flat pointer
@@ -381,8 +384,32 @@ struct StackT {
         return base[sp * BLK];
     }
 };
+// Basic tier, RT_STACK4B: 4-B entries -- a list flag and a 15-bit node / list
+// index, and the upper 16 bits of the entry distance (a positive f32 cut to
+// 16 bits is rounded down: the cull stays conservative; -inf stays -inf).
+// The block's stack takes half the LDS; the rest parks walk state.
+template <uint32_t CAP, uint32_t BLK>
+struct StackB4 {
+    RT_LDS uint32_t* base;
+    __device__ __forceinline__ void push(uint32_t sp, uint32_t ref, float t) {
+        const uint32_t r16 = (ref_kind(ref) == K_LIST ? 0x8000u : 0u) | (ref_index(ref) & 0x7fffu);
+        base[sp * BLK] = (r16 << 16) | (__float_as_uint(t) >> 16);
+    }
+    __device__ __forceinline__ uint2 at(uint32_t sp) const {
+        const uint32_t e = base[sp * BLK], r16 = e >> 16;
+        return make_uint2(make_ref((r16 & 0x8000u) ? K_LIST : K_BVH, r16 & 0x7fffu), e << 16);
+    }
+};
+template <int TIER, bool B4 = TIER == TIER_BASIC && RT_STACK4B>
+struct StackSel {
+    using type = StackT<lds_stack_entries(TIER), TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
+};
 template <int TIER>
-using StackFor = StackT<lds_stack_entries(TIER), TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
+struct StackSel<TIER, true> {
+    using type = StackB4<lds_stack_entries(TIER), RT_BLOCK_BASIC>;
+};
+template <int TIER>
+using StackFor = typename StackSel<TIER>::type;
 
 // Closest-hit state of one traversal: t and its f32 upper bound.
 struct Closest {
@@ -759,6 +786,39 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     }
 }
 
+// Basic tier with shading batches: a carried-over walk's state is parked in
+// LDS across the shading round (the ray-derived fields are made again).
+template <class Park>
+__device__ __forceinline__ void trace_park(const Trav<TIER_BASIC>& T, Park pk) {
+    constexpr uint32_t B = RT_BLOCK_BASIC;
+    const uint64_t c = (uint64_t)__double_as_longlong(T.cl.c), ht = (uint64_t)__double_as_longlong(T.hit.t);
+    pk[0 * B] = T.cur;
+    pk[1 * B] = T.sp | (T.pn << 8) | ((uint32_t)T.found << 16);
+    pk[2 * B] = (uint32_t)c;
+    pk[3 * B] = (uint32_t)(c >> 32);
+    pk[4 * B] = __float_as_uint(T.cl.c_f);
+    pk[5 * B] = (uint32_t)ht;
+    pk[6 * B] = (uint32_t)(ht >> 32);
+    pk[7 * B] = T.hit.ref;
+}
+template <class Park>
+__device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_BASIC>& T, Park pk) {
+    constexpr uint32_t B = RT_BLOCK_BASIC;
+    T.cur = pk[0 * B];
+    const uint32_t w = pk[1 * B];
+    T.sp = w & 0xffu;
+    T.pn = (w >> 8) & 0xffu;
+    T.found = (w >> 16) & 1u;
+    T.cl.c = __hiloint2double((int)pk[3 * B], (int)pk[2 * B]);
+    T.cl.c_f = __uint_as_float(pk[4 * B]);
+    T.hit.t = __hiloint2double((int)pk[6 * B], (int)pk[5 * B]);
+    T.hit.ref = pk[7 * B];
+    T.rf = make_rayf(wr);
+    T.a = len2(wr.d);
+    T.inva = 1.0 / T.a;
+    const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
+    T.sf = make_sphf(o, d);
+}
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
 template <int TIER>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
@@ -1754,6 +1814,16 @@ struct KParams {
 };
 
 template <int TIER>
+__device__ __forceinline__ StackFor<TIER> make_stack(RT_LDS uint2* s8, RT_LDS uint32_t* s4, RT_GLOBAL uint2* ovf,
+                                                     uint32_t stride) {
+    if constexpr (TIER == TIER_BASIC && RT_STACK4B)
+        return StackFor<TIER>{s4};
+    else
+        return StackFor<TIER>{s8, ovf, stride};
+}
+constexpr uint32_t RT_PARK_WORDS = 8;
+
+template <int TIER>
 __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : tier_full_bvh(TIER) ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
     // The params block is read-only for the launch: scalar loads, hoisted.
@@ -1762,13 +1832,23 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     uint32_t* queue = P->queue;
     constexpr int STACK = lds_stack_entries(TIER);
     constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
-    __shared__ uint2 stack_lds[STACK * BLK];
+    constexpr bool B4 = TIER == TIER_BASIC && RT_STACK4B;
+    __shared__ uint2 stack_lds[B4 ? 1 : STACK * BLK];
+    __shared__ uint32_t stack4_lds[B4 ? STACK * BLK : 1];
     __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
     RT_LDS uint4* med = (RT_LDS uint4*)(media_lds + threadIdx.x);
     __shared__ uint16_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * BLK : 1];
     RT_LDS uint16_t* pq = (RT_LDS uint16_t*)(pend_lds + threadIdx.x);
-    StackFor<TIER> stk{(RT_LDS uint2*)(stack_lds + threadIdx.x),
-                       P->stack_ovf + (uint64_t)blockIdx.x * BLK + threadIdx.x, gridDim.x * BLK};
+    StackFor<TIER> stk = make_stack<TIER>((RT_LDS uint2*)(stack_lds + threadIdx.x),
+                                          (RT_LDS uint32_t*)(stack4_lds + threadIdx.x),
+                                          P->stack_ovf + (uint64_t)blockIdx.x * BLK + threadIdx.x, gridDim.x * BLK);
+    // Basic tier with shading batches: the walk state of a lane whose walk
+    // carries over a shading round is parked here across it (RT_PARK_WORDS
+    // words: cur, sp | pn | found, c, c_f, hit t, hit ref), so that the
+    // shading code does not hold it in registers.
+    constexpr bool PARK = TIER == TIER_BASIC && RT_SHADE_BATCH_BASIC < 64;
+    __shared__ uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
+    RT_LDS uint32_t* pk = (RT_LDS uint32_t*)(park_lds + threadIdx.x);
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
     // 241 nodes for C1/C2), read by every node visit instead of global memory.
     __shared__ float4 node_lds[TIER == TIER_BASIC && RT_BVH4 ? NODE_LDS_CAP * 7 : 1];
@@ -1888,6 +1968,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             ++n_rays;
             trace_begin<TIER>(S, ray, T);
             walking = true;
+        } else if constexpr (PARK) {
+            trace_unpark(ray, T, pk);  // a walk carried over the last shading round
         }
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
@@ -1931,7 +2013,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         if constexpr (BATCH < 64 && tier_full(TIER)) {
             if (!walking) media_phase<TIER>(S, ray, T, stk, rng, med);
         }
-        if (BATCH < 64 && walking) continue;
+        if (BATCH < 64 && walking) {
+            if constexpr (PARK) trace_park(T, pk);
+            continue;
+        }
         bool panic = false;
         bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic);
         RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_b1;)
@@ -2106,7 +2191,11 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
                           rtk::F_NORMALMAP;
     if (features & rtk::F_GENERAL) return rtk::TIER_FULL_GL;
     if (features & full) return rtk::TIER_FULL;
-    if ((features & (rtk::F_PLANAR | rtk::F_REMAP)) || stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
+    if (features & (rtk::F_PLANAR | rtk::F_REMAP)) return rtk::TIER_MESH;
+    // the two-box tree's stack need; with 4-wide nodes the launcher decides on
+    // the 4-wide tree's (shallower: a 1 500-sphere world needs 22 entries as
+    // two-box nodes and fits the basic tier's 14 as 4-wide ones)
+    if (!RT_BVH4 && stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
     return rtk::TIER_BASIC;
 }
 

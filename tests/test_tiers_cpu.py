@@ -98,7 +98,15 @@ def test_small_sphere_bvhs(product, capi, rt, n):
     assert max(1, -(-(n - 1) // 3)) <= info.bvh_nodes <= max(1, n - 1)
 
 
-NODE_LDS_CAP = 32704 // 112  # RT_NODE_LDS_BYTES / sizeof(DNode4): the basic tier's LDS copy of the tree
+def _node_lds_cap():
+    """RT_NODE_LDS_BYTES / 112 (rt_kernel.h): the basic tier's LDS copy of the tree."""
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raytracer-2025_amd",
+                            "csrc", "rt_kernel.h")).read()
+    return int(re.search(r"#define RT_NODE_LDS_BYTES (\d+)", src).group(1)) // 112
+
+
+NODE_LDS_CAP = _node_lds_cap()
 
 
 @pytest.mark.parametrize("n", [600, 3000])
