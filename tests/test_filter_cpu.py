@@ -19,7 +19,7 @@ BUILD = os.path.join(HERE, "_build")
 
 def build(contract):
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "filter_prop_" + contract)
+    exe = os.path.join(BUILD, "filter_prop_%s.%d" % (contract, os.getpid()))  # one per pytest worker
     exact = os.path.join(BUILD, "sphere_exact.o")
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-c", os.path.join(HERE, "cpp", "sphere_exact.cpp"),
                     "-o", exact], check=True)

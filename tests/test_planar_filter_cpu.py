@@ -21,7 +21,7 @@ BUILD = os.path.join(HERE, "_build")
 
 def build(contract):
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "planar_prop_" + contract)
+    exe = os.path.join(BUILD, "planar_prop_%s.%d" % (contract, os.getpid()))  # one per pytest worker
     flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
     subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "planar_prop.cpp"), "-o", exe],
                    check=True)

@@ -24,7 +24,7 @@ def test_slab_is_conservative(contract, seed, fold, rcp):
     0: the widening applied per test.  rcp = 1: 1/d as an f32 quotient of d
     rounded to f32 (RT_RCP_F32) instead of the f64 quotient rounded once."""
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "slab_prop_%s_%d_%d" % (contract, fold, rcp))
+    exe = os.path.join(BUILD, "slab_prop_%s_%d_%d.%d" % (contract, fold, rcp, os.getpid()))  # one per pytest worker
     flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
     flags += ["-DRT_SLAB_FOLD=%d" % fold, "-DRT_RCP_F32=%d" % rcp]
     subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "slab_prop.cpp"), "-o", exe],
