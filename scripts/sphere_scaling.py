@@ -58,7 +58,8 @@ def world(s, n, seed=7):
 def main():
     spp = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     counts = [int(x) for x in sys.argv[2:]] or [100, 485, 900, 1500, 3000, 10000, 50000]
-    api = pkg.load()
+    lib = os.environ.get("RT_LIB")  # another build of the library (A/B), else the product's
+    api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", lib)), "rt_") if lib else pkg.load()
     torch.cuda.init()
     out = []
     for n in counts:
