@@ -16,12 +16,14 @@
 #endif
 // traversal-stack entries per lane; LDS = entries * block * 4 B
 #ifndef RT_STACK_BASIC
-#define RT_STACK_BASIC 14   // 56 KiB of the basic tier's 1024-lane block
+#define RT_STACK_BASIC 18   // 72 KiB of the basic tier's 1024-lane block
 #endif
 #ifndef RT_NODE_LDS_BYTES
-// basic tier: the world's 4-wide nodes in LDS, 804 of them (about 1 600
-// spheres): 160 KiB - 56 KiB of stack - 16 KiB of sphere queue, in 112-B nodes
-#define RT_NODE_LDS_BYTES 90048
+// basic tier: the world's 4-wide nodes in LDS, 658 of them: 160 KiB - 72 KiB
+// of stack - 16 KiB of sphere queue, in 112-B nodes.  With the 18-entry stack
+// sphere BVHs of up to about 1 200 spheres stay in the basic tier
+// (sphere-count scaling)
+#define RT_NODE_LDS_BYTES 73696
 #endif
 #define RT_STACK_MESH 16    // 32 KiB in LDS, deeper entries in a global overflow column
 #define RT_STACK_FULL 16    // (mesh and full tiers)
