@@ -36,6 +36,9 @@
 #ifndef RT_STACK_FLAT
 #define RT_STACK_FLAT 4     // full-flat tier (lists only: C3 needs 4); deeper ones overflow
 #endif
+#ifndef RT_FLAT_PARK_RAY
+#define RT_FLAT_PARK_RAY 1  // full-flat tier: the world ray too (read back where the walk needs it)
+#endif
 #ifndef RT_FLAT_LDS_STATE
 #define RT_FLAT_LDS_STATE 1 // full-flat tier: beta, L, acc and the item fields live in LDS across the walk
 #endif

@@ -819,10 +819,32 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_BASIC>& T,
     const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
     T.sf = make_sphf(o, d);
 }
+// The world-frame ray as the walk reads it: a register copy, or (full-flat
+// tier, RT_FLAT_PARK_RAY) the lane's LDS copy, read only where a walk step
+// needs it (leaving a Transform, the media phase) so that it holds no
+// registers across the walk.
+struct RayReg {
+    const Ray& r;
+    __device__ __forceinline__ Ray get() const { return r; }
+};
+struct RayLds {
+    const RT_LDS double* p;  // 7 doubles, RT_BLOCK apart: o, d, time
+    __device__ __forceinline__ Ray get() const {
+        Ray r;
+        r.o = d3(p[0 * RT_BLOCK], p[1 * RT_BLOCK], p[2 * RT_BLOCK]);
+        r.d = d3(p[3 * RT_BLOCK], p[4 * RT_BLOCK], p[5 * RT_BLOCK]);
+        r.time = p[6 * RT_BLOCK];
+        return r;
+    }
+};
+__device__ __forceinline__ RayReg world_ray(const Ray& r) { return RayReg{r}; }
+__device__ __forceinline__ const RayLds& world_ray(const RayLds& r) { return r; }
+
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
-template <int TIER>
-__device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
+template <int TIER, class WR>
+__device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Trav<TIER>& T, StackFor<TIER>& stk,
                                            const Rng& rng, RT_LDS uint4* med, Diag& dg) {
+    const auto wq = world_ray(wrr);
     constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
@@ -838,7 +860,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
         if (T.cur == REF_NONE) return false;
 #endif
     }
-    const Ray& r = FULL ? T.r : wr;
+    const Ray& r = FULL ? T.r : wq.get();
     uint32_t cur = T.cur;
     T.cur = REF_NONE;
     auto record = [&](uint32_t ref, double tt) {
@@ -970,7 +992,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
             }
             case K_POPXF: {
                 --T.nxf;
-                T.r = wr;
+                T.r = wq.get();
                 for (uint32_t k = 0; k < T.nxf; ++k) T.r = xf_ray(S.xforms[T.xfs.get(k)], T.r);
                 T.rf = make_rayf(T.r);
                 T.a = len2(T.r.d);
@@ -1004,12 +1026,13 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const Ray& wr, Tr
 
 // The queued media of a finished walk (FULL tier), each in its own frame,
 // against the walk's closest t; the walk's stack is free again.
-template <int TIER>
-__device__ __forceinline__ void media_phase(const SceneView& S, const Ray& wr, Trav<TIER>& T, StackFor<TIER>& stk,
+template <int TIER, class WR>
+__device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, Trav<TIER>& T, StackFor<TIER>& stk,
                                             const Rng& rng, const RT_LDS uint4* med) {
+    const auto wq = world_ray(wrr);
     for (uint32_t k = 0; k < T.nmed; ++k) {
         const uint4 e = med[k * RT_BLOCK];
-        Ray r = wr;
+        Ray r = wq.get();
         for (uint32_t j = 0; j < e.y; ++j) r = xf_ray(S.xforms[j == 0 ? e.z : e.w], r);
         double t;
         if (medium_hit<TIER != TIER_FULL_FLAT>(S, e.x, r, 1e-8, T.cl.c, stk, 0, rng, t)) {
@@ -1863,7 +1886,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     // item's fields) is parked in LDS across the walk, so that its registers
     // are free there instead of spilled to scratch around it.
     constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
-    __shared__ double pstate_lds[LDS_STATE ? 9 * RT_BLOCK : 1];
+    constexpr bool PARK_RAY = LDS_STATE && RT_FLAT_PARK_RAY;  // + the world ray (7 doubles)
+    __shared__ double pstate_lds[LDS_STATE ? (PARK_RAY ? 16 : 9) * RT_BLOCK : 1];
     __shared__ uint4 pitem_lds[LDS_STATE ? RT_BLOCK : 1];
     RT_LDS double* pst = (RT_LDS double*)(pstate_lds + threadIdx.x);
     RT_LDS uint4* pit = (RT_LDS uint4*)(pitem_lds + threadIdx.x);
@@ -1980,7 +2004,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 return trace4_step(S, ray, T, stk, pq, (const RT_LDS float4*)node_lds, dg);
             } else {
                 RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
-                return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                if constexpr (PARK_RAY)
+                    return trace_step<TIER>(S, RayLds{pst + 9 * RT_BLOCK}, T, stk, rng, med, dg);
+                else
+                    return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
             }
         };
         if constexpr (BATCH >= 64) {  // the whole wave finishes its walks, then shades
@@ -1989,12 +2016,21 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
                 pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
                 *pit = make_uint4(item, s_j, px, py);
+                if constexpr (PARK_RAY) {
+                    pst[9 * RT_BLOCK] = ray.o.x, pst[10 * RT_BLOCK] = ray.o.y, pst[11 * RT_BLOCK] = ray.o.z;
+                    pst[12 * RT_BLOCK] = ray.d.x, pst[13 * RT_BLOCK] = ray.d.y, pst[14 * RT_BLOCK] = ray.d.z;
+                    pst[15 * RT_BLOCK] = ray.time;
+                }
             }
             while (walking) walking = step();
             RT_DIAG_ONLY(const unsigned long long t_m0 = __builtin_amdgcn_s_memtime();)
-            if constexpr (tier_full(TIER)) media_phase<TIER>(S, ray, T, stk, rng, med);
+            if constexpr (PARK_RAY)
+                media_phase<TIER>(S, RayLds{pst + 9 * RT_BLOCK}, T, stk, rng, med);
+            else if constexpr (tier_full(TIER))
+                media_phase<TIER>(S, ray, T, stk, rng, med);
             RT_DIAG_ONLY(dg.cyc_media += __builtin_amdgcn_s_memtime() - t_m0;)
             if constexpr (LDS_STATE) {
+                if constexpr (PARK_RAY) ray = RayLds{pst + 9 * RT_BLOCK}.get();
                 beta = d3(pst[0 * RT_BLOCK], pst[1 * RT_BLOCK], pst[2 * RT_BLOCK]);
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
                 acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
