@@ -118,11 +118,6 @@ std::vector<double> params(const MtlRec& m, const char* key) {
     }
     return v;
 }
-bool file_exists(const std::string& p) {
-    std::ifstream f(p);
-    return (bool)f;
-}
-
 struct Model {
     std::string name;
     int material_id = -1;
