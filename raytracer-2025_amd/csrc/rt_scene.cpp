@@ -12,6 +12,10 @@
 
 #include "../../include/rt_mi355x.h"
 
+#ifndef RT_EXPAND_LEAF_LISTS
+#define RT_EXPAND_LEAF_LISTS 1  // lists of primitives under a BVH become BVH leaves (Flattener::collect_leaves)
+#endif
+
 namespace rth {
 
 static thread_local std::string g_error;
@@ -343,11 +347,21 @@ struct Flattener {
         return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
     }
 
+    // A list of plain primitives under a BVH (C5's ground boxes: six quads
+    // each) becomes leaves of that BVH too: the min over its children
+    // (hits.rs:34-46) is the BVH's closest hit over them (up to exact t ties,
+    // as for every rebuilt BVH), and the walk culls faces by their boxes
+    // instead of testing all of them.
+    static bool primitive(int kind) { return kind == O_SPHERE || kind == O_QUAD || kind == O_TRI || kind == O_MSPHERE; }
     void collect_leaves(int id, std::vector<int>& leaves) {
         const Obj& o = s->objs[id];
         if (o.kind == O_BVH && (o.hidden || leaves.empty())) {
             collect_leaves(o.left, leaves);
             if (o.right >= 0) collect_leaves(o.right, leaves);
+        } else if (RT_EXPAND_LEAF_LISTS && o.kind == O_LIST && !o.children.empty() &&
+                   std::all_of(o.children.begin(), o.children.end(),
+                               [&](int c) { return primitive(s->objs[c].kind); })) {
+            for (int c : o.children) leaves.push_back(c);
         } else {
             leaves.push_back(id);
         }
