@@ -347,6 +347,23 @@ struct Flattener {
         return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
     }
 
+    // an object that is a BVH or a list holding one (through nested lists)
+    bool holds_bvh(int id, int depth) const {
+        const Obj& o = s->objs[id];
+        if (o.kind == O_BVH) return true;
+        if (o.kind != O_LIST || depth >= 8) return false;
+        return std::any_of(o.children.begin(), o.children.end(), [&](int c) { return holds_bvh(c, depth + 1); });
+    }
+    // the elements of a list with nested lists opened, in order (the min of
+    // hits.rs:34-46 over nested lists is the min over their elements)
+    void list_elements(int id, std::vector<int>& out_ids, int depth) const {
+        const Obj& o = s->objs[id];
+        if (o.kind == O_LIST && depth < 8) {  // an empty list adds nothing (nothing to hit)
+            for (int c : o.children) list_elements(c, out_ids, depth + 1);
+        } else {
+            out_ids.push_back(id);
+        }
+    }
     // A list of plain primitives under a BVH (C5's ground boxes: six quads
     // each) becomes leaves of that BVH too: the min over its children
     // (hits.rs:34-46) is the BVH's closest hit over them (up to exact t ties,
@@ -486,11 +503,14 @@ struct Flattener {
                 // (up to exact t ties, as for every rebuilt BVH) -- without
                 // one walk iteration per element.  Lists of plain primitives
                 // (C3's Cornell box) stay lists: they keep the BVH-free tier.
+                // Nested lists (an OBJ's per-model BVHs beside C4's two
+                // spheres) join the rebuilt BVH element by element.
                 if (!reference_bvh && !no_collapse && o.children.size() >= 2 &&
-                    std::any_of(o.children.begin(), o.children.end(),
-                                [&](int c) { return s->objs[c].kind == O_BVH; })) {
+                    std::any_of(o.children.begin(), o.children.end(), [&](int c) { return holds_bvh(c, 0); })) {
+                    std::vector<int> elems;
+                    for (int c : o.children) list_elements(c, elems, 0);
                     std::vector<Item> items;
-                    for (int c : o.children) {
+                    for (int c : elems) {
                         auto e = emit(c, in_boundary, xf_depth);
                         Item x;
                         x.ref = e.first;
