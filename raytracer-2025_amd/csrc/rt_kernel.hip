@@ -81,7 +81,17 @@ struct Frame {
 // ------------------------------------------------------------------ textures
 // texture.rs: SolidColor 33-36, CheckerTexture 60-73, ImageTexture 165-174,
 // NoiseTexture 191-196 (+ perlin.rs), book-1 sky.
-__device__ double perlin_noise(const DPerlin& P, D3 p) {
+#ifndef RT_PERLIN_LDS
+#define RT_PERLIN_LDS 1
+#endif
+// Full tiers: the block's LDS copy of the world's first Perlin table (9 KiB,
+// copied at launch), read by NoiseTexture instead of global memory: the
+// marble's 7 octaves are 14 dependent table reads per shade, and a shading
+// batch with one marble hit waits for all of them.
+__shared__ DPerlin g_perlin_lds;
+
+template <class PP>
+__device__ double perlin_noise(PP P, D3 p) {
     const double fx = floor(p.x), fy = floor(p.y), fz = floor(p.z);
     const int64_t i = (int64_t)fx, j = (int64_t)fy, k = (int64_t)fz;
     const double u = p.x - fx, v = p.y - fy, w = p.z - fz;
@@ -90,9 +100,9 @@ __device__ double perlin_noise(const DPerlin& P, D3 p) {
     for (int di = 0; di < 2; ++di)
         for (int dj = 0; dj < 2; ++dj)
             for (int dk = 0; dk < 2; ++dk) {
-                const int idx = P.perm[0][(uint64_t)(i + di) & 255] ^ P.perm[1][(uint64_t)(j + dj) & 255] ^
-                                P.perm[2][(uint64_t)(k + dk) & 255];
-                const D3 c = d3(P.randvec[idx][0], P.randvec[idx][1], P.randvec[idx][2]);
+                const int idx = P->perm[0][(uint64_t)(i + di) & 255] ^ P->perm[1][(uint64_t)(j + dj) & 255] ^
+                                P->perm[2][(uint64_t)(k + dk) & 255];
+                const D3 c = d3(P->randvec[idx][0], P->randvec[idx][1], P->randvec[idx][2]);
                 const D3 wv = d3(u - di, v - dj, w - dk);
                 accum += (di * uu + (1 - di) * (1.0 - uu)) * (dj * vv + (1 - dj) * (1.0 - vv)) *
                          (dk * ww + (1 - dk) * (1.0 - ww)) * dot(c, wv);
@@ -144,7 +154,7 @@ __device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double 
     return (double)px[3];
 }
 
-template <bool FULL>
+template <bool FULL, bool PL = false>  // PL: NoiseTexture reads the LDS copy of the first Perlin table
 __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
     for (int guard = 0; guard < 16; ++guard) {
         const DTexture& t = S.textures[tid];
@@ -171,11 +181,12 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
                 return d3(px[0], px[1], px[2]);
             }
             case T_NOISE: {
-                const DPerlin& P = S.perlin[t.data];
+                const bool lds = PL && t.data == 0;
                 double accum = 0.0, weight = 1.0;
                 D3 tp = p;
                 for (int o = 0; o < 7; ++o) {
-                    accum += weight * perlin_noise(P, tp);
+                    accum += weight * (lds ? perlin_noise((const RT_LDS DPerlin*)&g_perlin_lds, tp)
+                                           : perlin_noise(S.perlin + t.data, tp));
                     tp = 2.0 * tp;
                     weight = 0.5 * weight;
                 }
@@ -1530,10 +1541,10 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
 #endif
 // A material's texture value; a SolidColor's colour comes with the material
 // record (MF_SOLID, set by the flatten), one dependent load fewer.
-template <bool FULL>
+template <bool FULL, bool PL = false>
 __device__ __forceinline__ D3 mat_tex(const SceneView& S, const DMaterial& M, double u, double v, D3 p) {
     if (RT_SOLID_ALBEDO && (M.flags & MF_SOLID)) return d3(M.albedo[0], M.albedo[1], M.albedo[2]);
-    return tex_value<FULL>(S, M.tex, u, v, p);
+    return tex_value<FULL, PL>(S, M.tex, u, v, p);
 }
 
 // vec3.rs:313-322
@@ -1563,7 +1574,7 @@ template <int D>
 __device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p) {
     const DMaterial& M = S.materials[mid];
     if (M.type == M_DIFFUSE_LIGHT) {
-        const D3 self = mat_tex<true>(S, M, u, v, p);
+        const D3 self = mat_tex<true, RT_PERLIN_LDS>(S, M, u, v, p);
         D3 inner = d3(0.0, 0.0, 0.0);
         if constexpr (D > 0)
             if (M.inner >= 0) inner = emitted_tree<D - 1>(S, M.inner, u, v, p);
@@ -1585,6 +1596,7 @@ template <int TIER>
 __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
                                       const HitInfo& h, bool& panic) {
     constexpr bool FULL = tier_full(TIER);
+    constexpr bool PL = tier_full_bvh(TIER) && RT_PERLIN_LDS;  // the flat tier's LDS is full
     uint32_t ovf = 0;
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
@@ -1599,7 +1611,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 u = phi / (2.0 * PI);
                 v = theta / PI;
             }
-            L = L + beta * tex_value<FULL>(S, S.background_tex, u, v, p);
+            L = L + beta * tex_value<FULL, PL>(S, S.background_tex, u, v, p);
         }
         return true;
     }
@@ -1634,12 +1646,12 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
         if (M.flags & MF_EMISSIVE) {
             D3 em;
             if (M.type == M_DIFFUSE_LIGHT) {
-                em = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
+                em = mat_tex<FULL, PL>(S, M, rec.u, rec.v, rec.p);
             } else {  // Mix of non-wrapping materials (flatten checks)
                 const DMaterial& A = S.materials[M.inner];
                 const DMaterial& B = S.materials[M.inner2];
-                const D3 ea = A.type == M_DIFFUSE_LIGHT ? mat_tex<FULL>(S, A, rec.u, rec.v, rec.p) : d3(0, 0, 0);
-                const D3 eb = B.type == M_DIFFUSE_LIGHT ? mat_tex<FULL>(S, B, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                const D3 ea = A.type == M_DIFFUSE_LIGHT ? mat_tex<FULL, PL>(S, A, rec.u, rec.v, rec.p) : d3(0, 0, 0);
+                const D3 eb = B.type == M_DIFFUSE_LIGHT ? mat_tex<FULL, PL>(S, B, rec.u, rec.v, rec.p) : d3(0, 0, 0);
                 em = ((1.0 - M.fuzz) * ea) + (M.fuzz * eb);
             }
             L = L + beta * em;
@@ -1659,7 +1671,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     D3 albedo = d3(0, 0, 0);
     switch (M.type) {
         case M_LAMBERTIAN:  // material.rs:60-65
-            albedo = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
+            albedo = mat_tex<FULL, PL>(S, M, rec.u, rec.v, rec.p);
             pdf_kind = 0;
             break;
         case M_EMPTY:  // material.rs:41-46
@@ -1707,14 +1719,14 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 if (isnan(pl)) panic = true;
                 dir = perp + (-pl * n);
             }
-            beta = beta * mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
+            beta = beta * mat_tex<FULL, PL>(S, M, rec.u, rec.v, rec.p);
             ray = Ray{rec.p, dir, ray.time};
             break;
         }
         default:
             if constexpr (FULL) {
                 if (M.type == M_ISOTROPIC) {  // material.rs:199-206
-                    albedo = mat_tex<FULL>(S, M, rec.u, rec.v, rec.p);
+                    albedo = mat_tex<FULL, PL>(S, M, rec.u, rec.v, rec.p);
                     pdf_kind = 1;
                     break;
                 }
@@ -1880,6 +1892,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
         for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) node_lds[k] = src[k];
         __syncthreads();
+    }
+    if constexpr (tier_full_bvh(TIER) && RT_PERLIN_LDS) {
+        if (S.n_perlin > 0) {
+            const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.perlin);
+            RT_LDS float4* dst = (RT_LDS float4*)&g_perlin_lds;
+            for (uint32_t k = threadIdx.x; k < sizeof(DPerlin) / 16; k += BLK) dst[k] = src[k];
+            __syncthreads();
+        }
     }
     const uint32_t lane = __lane_id();
     // Full-flat tier: the path state the walk never reads (beta, L, acc, the

@@ -234,6 +234,8 @@ struct SceneView {
     uint32_t stack_need;     // max traversal stack entries (host-computed)
     uint32_t features;       // F_* of everything reachable from world/lights
     uint32_t n_nodes4;       // entries of nodes4
+    uint32_t n_perlin;       // entries of perlin (the full tiers copy the first into LDS)
+    uint32_t pad_;
 };
 
 // Scene features; the launcher picks the smallest kernel tier covering them.

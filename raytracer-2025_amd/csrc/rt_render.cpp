@@ -316,6 +316,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.stack_need = hw.stack_need;
     v.features = hw.features;
     v.n_nodes4 = (uint32_t)hw.nodes4.size();
+    v.n_perlin = (uint32_t)hw.perlin.size();
     fw.tier = tier;
     fw.stack_need = hw.stack_need;
     fw.n_prims = hw.n_prims;
