@@ -260,6 +260,9 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
     return true;
 }
 
+#ifndef RT_UV_ON_DEMAND
+#define RT_UV_ON_DEMAND 1  // a planar hit's (u, v) only when its material or remap reads them
+#endif
 #ifndef RT_PLANAR_EARLY
 // 1: decide early, with the same outcome as the full test: t = num / denom
 // rounded is negative when num and denom have opposite signs (num != 0), so
@@ -1312,11 +1315,18 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     } else if (kind == K_QUAD || kind == K_TRI) {
         const DPlanar& P = S.planars[idx];
         outward = d3(P.f[0], P.f[1], P.f[2]);
-        const D3 hv = p - d3(P.f[4], P.f[5], P.f[6]);
-        const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
-        rec.u = dot(w, cross(hv, v));
-        rec.v = dot(w, cross(u, hv));
         rec.mat = S.planar_mat[idx];
+        // (u, v) = (alpha, beta) of quad.rs:93-99, for a texture that reads
+        // them or an OBJ triangle's RemappedMaterial (obj.rs:32-62); nothing
+        // else looks at them (full tiers: C3 -1.3 %, C5 -2 %; the mesh tier's
+        // OBJ triangles always need them)
+        if (!RT_UV_ON_DEMAND || !FULL || (S.materials[rec.mat].flags & MF_NEEDS_UV) ||
+            (PLANAR && kind == K_TRI && S.planar_remap[idx] >= 0)) {
+            const D3 hv = p - d3(P.f[4], P.f[5], P.f[6]);
+            const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
+            rec.u = dot(w, cross(hv, v));
+            rec.v = dot(w, cross(u, hv));
+        }
     } else {  // K_MEDIUM (volume.rs:67-72)
         outward = d3(1.0, 0.0, 0.0);
         rec.mat = S.media[idx].phase_mat;
