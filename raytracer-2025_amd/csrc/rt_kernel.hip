@@ -62,6 +62,14 @@ __device__ unsigned long long g_diag[16];
 #define RT_DIAG_ONLY(x)
 #endif
 
+#ifdef RT_WAVE_TRACE
+// trace build: per lane of the grid, {start, end (s_memrealtime, 100 MHz),
+// queue entries taken, rays traced, time / queue entry / rays so far at the
+// lane's last refill} (scripts/lane_trace.py)
+constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 8;
+__device__ unsigned long long g_lane_trace[RT_TRACE_LANES * RT_TRACE_W];
+#endif
+
 struct Ray {
     D3 o, d;
     double time;
@@ -73,10 +81,29 @@ struct Frame {
     uint32_t max_depth;
     uint32_t key0, key1;
     uint32_t total_items;
+    // Work queue: entry q = part q % parts of stratum row q / parts (item);
+    // a part traces part_len consecutive samples s_j (the last part the rest)
+    // and writes their f64 sum to partial[q]; the reduce adds a row's parts in
+    // order.  A launch ends on its longest queue entries, and a whole row of a
+    // pixel whose paths bounce 40 times inside a glass sphere is ~10 ms of one
+    // wave (scripts/lane_trace.py): parts keep the last entries short.
+    uint32_t parts, part_len, queue_total;
+    uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
+    // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
+    // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
+    double inv_parts, inv_S, inv_W;
+    float inv_guide;
     uint32_t defocus;
     double recip_sqrt_spp, pixel_sample_scale;
     D3 center, pixel00, du, dv, disk_u, disk_v;
 };
+
+// n / d for n < 2^32, d < 2^20, from inv = 1/d rounded up: n * inv is at least
+// the quotient's integer part when d divides n (a representable product,
+// rounded to nearest, cannot fall below it) and below the next integer
+// otherwise (the excess n * 2^-52 / d stays under 1/d): three f64 / convert
+// instructions instead of a ~25-instruction integer division expansion.
+__device__ __forceinline__ uint32_t udiv_inv(uint32_t n, double inv) { return (uint32_t)((double)n * inv); }
 
 // ------------------------------------------------------------------ textures
 // texture.rs: SolidColor 33-36, CheckerTexture 60-73, ImageTexture 165-174,
@@ -1066,6 +1093,12 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #ifndef RT_DEFER_THRESH
 #define RT_DEFER_THRESH 48  // lanes with a queued sphere that trigger a sphere round
 #endif
+#ifndef RT_DEFER_REL
+// ... or 3/4 of the lanes still in the walk, when fewer than 64 are: a wave
+// thinned out at the end of a launch tests its queued spheres instead of
+// walking on unbounded until none of its lanes can
+#define RT_DEFER_REL 1
+#endif
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
@@ -1212,7 +1245,13 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const bool can = (T.cur != REF_NONE || T.sp > 0) && pn <= ROOM;
     const unsigned long long mw0 = __ballot(can);
     const unsigned long long mp0 = __ballot(pn > 0);
-    const bool round = (mw0 == 0 || __popcll(mp0) >= RT_DEFER_THRESH) && pn > 0;
+#if RT_DEFER_REL
+    const uint32_t in_walk = (uint32_t)__popcll(__ballot(true));
+    const uint32_t thresh = min((uint32_t)RT_DEFER_THRESH, (in_walk * 3u + 3u) / 4u);
+#else
+    constexpr uint32_t thresh = RT_DEFER_THRESH;
+#endif
+    const bool round = (mw0 == 0 || (uint32_t)__popcll(mp0) >= thresh) && pn > 0;
     // the loads are unconditional (a lane without a round / a node reads
     // entry 0, cache-hot) so that no branch stands between them and their
     // waits: the sphere test then waits for its own load only
@@ -1853,7 +1892,7 @@ struct KParams {
     SceneView S;
     Frame F;
     uint32_t* queue;
-    double* partial;
+    double* partial;  // [queue_total][3]: the f64 sum of each queue entry's samples
     unsigned long long* stats;
     RT_GLOBAL uint2* stack_ovf;  // mesh / full tiers: [stack_need - LDS entries][grid * RT_BLOCK]
 };
@@ -1925,7 +1964,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     Rng rng;
     rng.k0 = F.key0;
     rng.k1 = F.key1;
-    uint32_t item = 0, s_j = 0, px = 0, py = 0;
+    // the lane's queue entry q: stratum row s_i of pixel (px, py), samples s_j ..< s_end
+    uint32_t q = 0, s_i = 0, s_j = 0, s_end = 0, px = 0, py = 0;
     bool need = true;
     bool in_path = false;
     Ray ray;
@@ -1937,6 +1977,12 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     Diag dg;
     Trav<TIER> T;
     bool walking = false;
+#ifdef RT_WAVE_TRACE
+    const uint32_t trace_lane = blockIdx.x * BLK + threadIdx.x;
+    const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t trace_items = 0, trace_q = 0, trace_rays = 0;
+    unsigned long long trace_tq = trace_t0;
+#endif
     for (;;) {
         RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
         // ---- refill: wave-aggregated dequeue of stratum rows.  The wave takes
@@ -1950,13 +1996,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             uint32_t fresh = 0;
             // guided chunk: about 1/GUIDE of the items left (as last seen) per
             // wave of the grid, so the last chunks are small and waves finish
-            // together; never below 64 (one item per lane)
+            // together; never below what the wave's lanes need now, nor below
+            // Frame::chunk_min.  Near the end a wave takes only what its lanes
+            // need: a pool held by a slow wave (deep glass paths) is work the
+            // idle waves cannot take (scripts/lane_trace.py).
             uint32_t chunk = RT_QUEUE_CHUNK;
 #if RT_QUEUE_GUIDE
             {
-                const uint32_t left = F.total_items > pool_end ? F.total_items - pool_end : 0u;
-                const uint32_t g = left / (gridDim.x * (BLK / 64) * RT_QUEUE_GUIDE);
-                chunk = g < 64u ? 64u : (g > (uint32_t)RT_QUEUE_CHUNK ? (uint32_t)RT_QUEUE_CHUNK : g);
+                const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
+                const uint32_t g = max((uint32_t)((float)left * F.inv_guide), F.chunk_min);
+                chunk = max(min(g, (uint32_t)RT_QUEUE_CHUNK), avail < n ? n - avail : 0u);
             }
 #endif
             if (avail < n) {
@@ -1974,20 +2023,29 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if (need) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                item = rank < avail ? old_next + rank : fresh + (rank - avail);
-                if (item >= F.total_items) break;
+                q = rank < avail ? old_next + rank : fresh + (rank - avail);
+                if (q >= F.queue_total) break;
                 need = false;
-                s_j = 0;
+#ifdef RT_WAVE_TRACE
+                ++trace_items;
+                trace_q = q;
+                trace_rays = n_rays;
+                trace_tq = __builtin_amdgcn_s_memrealtime();
+#endif
+                const uint32_t item = udiv_inv(q, F.inv_parts);
+                s_j = (q - item * F.parts) * F.part_len;
+                s_end = min(F.S, s_j + F.part_len);
                 acc = d3(0, 0, 0);
-                const uint32_t pl = item / F.S;
-                px = pl % F.W;
-                py = F.row_offset + (pl / F.W) * F.row_stride;
+                const uint32_t pl = udiv_inv(item, F.inv_S);
+                s_i = item - pl * F.S;
+                const uint32_t prow = udiv_inv(pl, F.inv_W);
+                px = pl - prow * F.W;
+                py = F.row_offset + prow * F.row_stride;
                 rng.pixel = py * F.W + px;
             }
         }
         if (!in_path) {
             // ---- Camera::get_ray (camera.rs:247-273), vertex 0
-            const uint32_t s_i = item % F.S;
             rng.sample = s_i * F.S + s_j;
             rng.begin(0);
             uint32_t ovf = 0;
@@ -2045,7 +2103,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pst[0 * RT_BLOCK] = beta.x, pst[1 * RT_BLOCK] = beta.y, pst[2 * RT_BLOCK] = beta.z;
                 pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
                 pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
-                *pit = make_uint4(item, s_j, px, py);
+                *pit = make_uint4(q, s_i | (s_end << 16), s_j, px | (py << 16));
                 if constexpr (PARK_RAY) {
                     pst[9 * RT_BLOCK] = ray.o.x, pst[10 * RT_BLOCK] = ray.o.y, pst[11 * RT_BLOCK] = ray.o.z;
                     pst[12 * RT_BLOCK] = ray.d.x, pst[13 * RT_BLOCK] = ray.d.y, pst[14 * RT_BLOCK] = ray.d.z;
@@ -2065,7 +2123,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
                 acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
                 const uint4 it = *pit;
-                item = it.x, s_j = it.y, px = it.z, py = it.w;
+                q = it.x, s_i = it.y & 0xFFFFu, s_end = it.y >> 16, s_j = it.z, px = it.w & 0xFFFFu, py = it.w >> 16;
             }
         } else {
             const unsigned long long active = __ballot(true);
@@ -2102,8 +2160,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             acc = acc + L;
             in_path = false;
             ++s_j;
-            if (s_j == F.S) {
-                double* dst = P->partial + (uint64_t)item * 3;
+            if (s_j == s_end) {
+                double* dst = P->partial + (uint64_t)q * 3;
                 dst[0] = acc.x;
                 dst[1] = acc.y;
                 dst[2] = acc.z;
@@ -2129,6 +2187,19 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     atomicAdd(&g_diag[10], dg.loads);
     atomicAdd(&g_diag[11], dg.pops);
     atomicAdd(&g_diag[12], dg.pop_reads);
+#endif
+#ifdef RT_WAVE_TRACE
+    if (trace_lane < RT_TRACE_LANES) {
+        unsigned long long* t = g_lane_trace + (uint64_t)trace_lane * RT_TRACE_W;
+        t[0] = trace_t0;
+        t[1] = __builtin_amdgcn_s_memrealtime();
+        t[2] = trace_items;
+        t[3] = n_rays;
+        t[4] = trace_tq;
+        t[5] = trace_q;
+        t[6] = trace_rays;
+        t[7] = 0;
+    }
 #endif
     atomicAdd(&P->stats[0], (unsigned long long)n_rays);
     if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
@@ -2165,6 +2236,13 @@ RT_TIER_ENTRY(3)
 #endif
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 4
 RT_TIER_ENTRY(4)
+#endif
+#if defined(RT_WAVE_TRACE)
+extern "C" int rt_lane_trace(unsigned long long* out, uint64_t n_lanes) {
+    if (n_lanes > rtk::RT_TRACE_LANES) n_lanes = rtk::RT_TRACE_LANES;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_lane_trace),
+                                    n_lanes * rtk::RT_TRACE_W * sizeof(unsigned long long));
+}
 #endif
 #if defined(RT_DIAG)
 // diagnostic build: the counters live with the (DIAG_TIER) kernel that adds to them
@@ -2206,20 +2284,28 @@ __device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
     return (uint8_t)(q < 0.0 ? 0.0 : (q > 255.0 ? 255.0 : q));
 }
 
-// Sums the S stratum rows of each pixel in s_i order, * pixel_sample_scale,
+// Sums the S stratum rows of each pixel in s_i order -- a row = its `parts`
+// part sums added in part order -- * pixel_sample_scale,
 // to linear f32 (camera.rs:193), and -- when srgb is given -- the pixel's
 // to_rgb bytes from the f64 sum, as the reference converts its f64 color.
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
-                                                       double scale, float* __restrict__ out,
+                                                       uint32_t parts, double scale, float* __restrict__ out,
                                                        uint8_t* __restrict__ srgb, int toon) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
-    const double* src = partial + (uint64_t)p * S * 3;
+    const double* src = partial + (uint64_t)p * S * parts * 3;
     double r = 0.0, g = 0.0, b = 0.0;
     for (uint32_t k = 0; k < S; ++k) {
-        r += src[k * 3 + 0];
-        g += src[k * 3 + 1];
-        b += src[k * 3 + 2];
+        const double* row = src + k * parts * 3;
+        double rr = row[0], rg = row[1], rb = row[2];
+        for (uint32_t j = 1; j < parts; ++j) {
+            rr += row[j * 3 + 0];
+            rg += row[j * 3 + 1];
+            rb += row[j * 3 + 2];
+        }
+        r += rr;
+        g += rg;
+        b += rb;
     }
     out[(uint64_t)p * 3 + 0] = (float)(r * scale);
     out[(uint64_t)p * 3 + 1] = (float)(g * scale);
@@ -2291,6 +2377,15 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.key0 = (uint32_t)fd->seed;
     F.key1 = (uint32_t)(fd->seed >> 32);
     F.total_items = fd->W * fd->rows * fd->S;
+    F.parts = fd->parts > 1 ? fd->parts : 1u;  // the host's rtk_row_parts: no part empty
+    F.part_len = (fd->S + F.parts - 1) / F.parts;
+    F.queue_total = F.total_items * F.parts;
+    F.chunk_min = fd->chunk_min;
+    auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
+    F.inv_parts = inv_up(F.parts);
+    F.inv_S = inv_up(F.S);
+    F.inv_W = inv_up(F.W);
+    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
     F.pixel_sample_scale = fd->pixel_sample_scale;
@@ -2319,7 +2414,7 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
-                       fd->pixel_sample_scale, out, srgb, toon);
+                       F.parts, fd->pixel_sample_scale, out, srgb, toon);
     return hipGetLastError();
 }
 
@@ -2336,6 +2431,17 @@ extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rtk::rt_to_rgb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, lin, srgb, n, toon);
     return hipGetLastError();
+}
+
+extern "C" uint32_t rtk_row_parts(uint32_t W, uint32_t H, uint32_t S, uint32_t part_samples, uint64_t budget_bytes) {
+    if (part_samples == 0 || S <= part_samples) return 1;
+    uint32_t parts = (S + part_samples - 1) / part_samples;
+    // within the part-sum budget, and the queue of the whole frame below 2^32 entries
+    while (parts > 1 && ((uint64_t)W * H * S * parts * 3 * sizeof(double) > budget_bytes ||
+                         (uint64_t)W * H * S * parts >= 0xFFF00000ull))
+        --parts;
+    const uint32_t len = (S + parts - 1) / parts;
+    return (S + len - 1) / len;  // as many parts of that length as S takes: none empty
 }
 
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -122,7 +123,7 @@ struct DeviceWorld {
     // the last render on this slot
     bool ran = false;  // the path kernel ran (ev_start / ev_stop are valid)
     uint64_t samples = 0;
-    uint32_t W = 0, rows = 0, S = 0;
+    uint32_t W = 0, rows = 0, S = 0, parts = 1;
     hipStream_t last_stream = nullptr;
 };
 
@@ -433,6 +434,7 @@ static int32_t init_frame(const rt_camera* c, uint64_t seed, uint32_t row_offset
     f.pixel_sample_scale = 1.0 / (double)(f.S * f.S);
     f.recip_sqrt_spp = 1.0 / (double)f.S;
     if ((uint64_t)W * f.rows * f.S >= 0xFFF00000ull) return set_error(RT_EINVAL, "frame too large for one launch");
+    if (W >= (1u << 20)) return set_error(RT_EINVAL, "image_width must be below 2^20");
     V3 from(c->look_from), at(c->look_at), up(c->vec_up);
     double theta = c->vertical_fov_in_degrees * (PI / 180.0);
     double h = std::tan(theta / 2.0);
@@ -494,6 +496,15 @@ struct Part {
     double flatten_ms = 0;
 };
 
+// A tuning knob from the environment (A/B runs), else its default.
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    char* end = nullptr;
+    const unsigned long x = std::strtoul(v, &end, 10);
+    return (end && *end == 0 && x <= 0xFFFFFFFFul) ? (uint32_t)x : dflt;
+}
+
 // Runs on the part's host thread: device world, buffers, kernel launch.
 static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights, const rt_camera* cam, uint64_t seed,
                      bool reference_bvh, FlatWorld& fw, Part& p) {
@@ -512,7 +523,13 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     rtk_frame_desc f;
     if ((rc = init_frame(cam, seed, p.row_offset, p.row_stride, f)) != RT_OK) return fail(rc);
     p.rows = f.rows;
-    if ((rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * 3 * sizeof(double),
+    // Every stratum row goes out in parts of about RT_PART_SAMPLES (4) samples
+    // (rtk_row_parts; decided on the whole frame, so shards and device counts
+    // sum rows alike): a launch ends on its longest queue entries.
+    f.parts = rtk_row_parts(f.W, rt_camera_image_height(cam), f.S, env_u32("RT_PART_SAMPLES", 4),
+                            (uint64_t)env_u32("RT_PART_BUDGET_MB", 8192) << 20);
+    f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
+    if ((rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * f.parts * 3 * sizeof(double),
                    "hipMalloc partial sums")) != RT_OK)
         return fail(rc);
     if (!p.out &&
@@ -555,6 +572,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     d->W = f.W;
     d->rows = f.rows;
     d->S = f.S;
+    d->parts = f.parts;
     d->last_stream = p.stream;
 }
 
@@ -859,8 +877,28 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
     (void)hipSetDevice(d->device);
     hipError_t e = hipStreamSynchronize(d->last_stream);
     if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
-    if (n && (e = hipMemcpy(out, d->partial, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
+    if (d->parts <= 1) {
+        if (n && (e = hipMemcpy(out, d->partial, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy partials");
+        return RT_OK;
+    }
+    // rows traced in parts: a row's sum = its part sums added in part order,
+    // as rt_reduce_kernel adds them
+    std::vector<double> parts;
+    try {
+        parts.resize(n * d->parts);
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
+    if ((e = hipMemcpy(parts.data(), d->partial, parts.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "hipMemcpy partials");
+    for (uint64_t row = 0; row < n / 3; ++row)
+        for (int c = 0; c < 3; ++c) {
+            const double* src = parts.data() + row * d->parts * 3 + c;
+            double sum = src[0];
+            for (uint32_t j = 1; j < d->parts; ++j) sum += src[j * 3];
+            out[row * 3 + c] = sum;
+        }
     return RT_OK;
 }
 

@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Lane trace (GPU box): renders a workload's row shard with
+librt_mi355x_trace.so (-DRT_WAVE_TRACE: per lane of the grid, s_memrealtime at
+start and exit, queue entries taken, rays) and prints how the launch ends --
+when lanes start and finish relative to the kernel's span, and how many lanes
+are still working in each tenth of it.
+  python scripts/lane_trace.py [workload] [spp] [row_stride ...]"""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime: load torch first)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+capi = importlib.import_module("raytracer-2025_amd.capi")
+rt = importlib.import_module("raytracer-2025_amd.raytracer")
+scenes = importlib.import_module("raytracer-2025_amd.scenes")
+import bench  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    spp = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl][1]
+    strides = [int(x) for x in sys.argv[3:]] or [1, 8]
+    torch.cuda.init()
+    lib = ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", os.environ.get("TRACE_LIB", "librt_mi355x_trace.so")))
+    lib.rt_lane_trace.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint64]
+    api = capi.Api(lib, "rt_")
+    s = rt.Scene(api)
+    world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
+    cam.render(world, lights, seed=1, want_srgb=False)
+    n = 1 << 19
+    buf = (ctypes.c_ulonglong * (n * 8))()
+    for stride in strides:
+        ctypes.memset(buf, 0, ctypes.sizeof(buf))
+        torch.cuda.synchronize()
+        _, _, st = cam.render(world, lights, seed=1, row_stride=stride, want_srgb=False)
+        assert lib.rt_lane_trace(buf, n) == 0
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8).astype(np.int64)
+        a = a[a[:, 1] > 0]
+        t0, t1 = a[:, 0].min(), a[:, 1].max()
+        span = (t1 - t0) / 100.0  # 100 MHz -> us
+        end = (a[:, 1] - t0) / 100.0
+        start = (a[:, 0] - t0) / 100.0
+        tenth = [float(np.mean(end > span * k / 10.0)) for k in range(10)]
+        rec = {
+            "workload": desc, "spp": spp, "row_stride": stride, "lanes": int(len(a)),
+            "kernel_ms": round(st.kernel_ms, 3), "trace_span_ms": round(span / 1e3, 3),
+            "start_us_max": round(float(start.max()), 1),
+            "end_ms_pct": {p: round(float(np.percentile(end, p)) / 1e3, 3) for p in (1, 10, 50, 90, 99, 100)},
+            "lanes_working_at_tenths": [round(x, 4) for x in tenth],
+            "busy_fraction": round(float(np.sum(end - start) / (len(a) * span)), 4),
+            "entries_per_lane": {"min": int(a[:, 2].min()), "mean": round(float(a[:, 2].mean()), 2),
+                                 "max": int(a[:, 2].max())},
+            "rays_per_lane": {"min": int(a[:, 3].min()), "mean": round(float(a[:, 3].mean()), 1),
+                              "max": int(a[:, 3].max())},
+        }
+        # the last lanes to finish: when they took their last queue entry, which
+        # one (pixel row of the shard, stratum row / part), rays since then
+        S = cam.sqrt_spp
+        last = np.argsort(a[:, 1])[-8:][::-1]
+        rec["last_lanes"] = [{"end_ms": round((a[i, 1] - t0) / 1e5, 3), "last_entry_ms": round((a[i, 4] - t0) / 1e5, 3),
+                              "q": int(a[i, 5]), "pixel": int(a[i, 5] // S), "rays_after": int(a[i, 3] - a[i, 6]),
+                              "entries": int(a[i, 2])} for i in last]
+        rec["last_entry_ms_pct"] = {p: round(float(np.percentile((a[:, 4] - t0) / 1e5, p)), 3) for p in (50, 99, 100)}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Strong-scaling rehearsal on one GPU (GPU box): the row shard one rank of an
+N-GPU run renders (rows r, r + N, ...; rt_render_opts row_offset / row_stride)
+timed alone, for N = 1, 2, 4, 8 and every r of the largest N.  The kernel time
+of a shard against 1/N of the whole frame's is the part of the 8-GPU scaling
+loss that lives in the kernel (the launch tail of a smaller grid of work); the
+gather (rt_stats.gather_ms, ~20 us at N = 8) and RCCL set-up are not in it.
+  python scripts/shard_scaling.py [workload] [spp] [reps]"""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+import torch  # noqa: F401  (one HIP runtime: load torch first)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+rt = importlib.import_module("raytracer-2025_amd.raytracer")
+scenes = importlib.import_module("raytracer-2025_amd.scenes")
+pkg = importlib.import_module("raytracer-2025_amd")
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (the workloads)
+
+
+def main():
+    wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    spp = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl][1]
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    lib = os.environ.get("RT_LIB")
+    api = pkg.load() if not lib else importlib.import_module("raytracer-2025_amd.capi").Api(
+        ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", lib)), "rt_")
+    torch.cuda.init()
+    s = rt.Scene(api)
+    world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
+    cam.render(world, lights, seed=1, want_srgb=False)  # flatten + upload
+    full = None
+    out = []
+    for n in (1, 2, 4, 8):
+        for r in (range(n) if n == 8 else (0,)):
+            best = None
+            for _ in range(reps):
+                _, _, st = cam.render(world, lights, seed=1, row_offset=r, row_stride=n, want_srgb=False)
+                best = st.kernel_ms if best is None else min(best, st.kernel_ms)
+            if n == 1:
+                full = best
+            rec = {"n": n, "rank": r, "kernel_ms": round(best, 3), "samples": int(st.samples),
+                   "eff_vs_1": round(full / (n * best), 4)}
+            print(json.dumps(rec), flush=True)
+            out.append(rec)
+    worst8 = max(x["kernel_ms"] for x in out if x["n"] == 8)
+    print(json.dumps({"workload": desc, "spp": spp, "reps": reps, "full_ms": full,
+                      "eff8_worst_rank": round(full / (8 * worst8), 4), "runs": out}))
+
+
+if __name__ == "__main__":
+    main()

@@ -49,10 +49,14 @@ int main(int argc, char** argv) {
         // the sphere at its origin, or aimed at the sphere's rim
         double o[3], d[3], nrm[3];
         unit(nrm);
-        const int ok = (int)(U(rng) * 4);
+        const int ok = (int)(U(rng) * 5);
         const double lift = ok == 1 ? (U(rng) - 0.5) * 1e-6 * r : 0.0;
         if (ok <= 1) for (int k = 0; k < 3; ++k) o[k] = c[k] + (r + lift) * nrm[k];
         else if (ok == 2) { o[0] = 13; o[1] = 2; o[2] = 3; }
+        else if (ok == 4) {  // inside: anywhere from the center to a hair below the surface
+            const double f = U(rng) < 0.5 ? U(rng) : 1.0 - std::exp(std::log(1e-12) + U(rng) * std::log(1e10));
+            for (int k = 0; k < 3; ++k) o[k] = c[k] + f * r * nrm[k];
+        }
         else for (int k = 0; k < 3; ++k) o[k] = c[k] + (U(rng) - 0.5) * 40 * (r + 1);
         const int dk = (int)(U(rng) * 3);
         unit(d);
