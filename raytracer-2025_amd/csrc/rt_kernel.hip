@@ -81,10 +81,11 @@ struct Frame {
     uint32_t max_depth;
     uint32_t key0, key1;
     uint32_t total_items;
-    // Work queue: entry q = part q % parts of stratum row q / parts (item);
-    // a part traces part_len consecutive samples s_j (the last part the rest)
-    // and writes their f64 sum to partial[q]; the reduce adds a row's parts in
-    // order.  A launch ends on its longest queue entries, and a whole row of a
+    // Work queue: entry q = part q % parts of stratum row q / parts (item =
+    // launch pixel * S + s_i); a part traces part_len consecutive samples s_j
+    // (the last part the rest) and writes their f64 sum to partial slot
+    // (s_i * parts + part) * pixels + pixel -- pixel-minor, so that the reduce
+    // reads coalesced -- and the reduce adds a row's parts in order.  A launch ends on its longest queue entries, and a whole row of a
     // pixel whose paths bounce 40 times inside a glass sphere is ~10 ms of one
     // wave (scripts/lane_trace.py): parts keep the last entries short.
     uint32_t parts, part_len, queue_total;
@@ -1964,8 +1965,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     Rng rng;
     rng.k0 = F.key0;
     rng.k1 = F.key1;
-    // the lane's queue entry q: stratum row s_i of pixel (px, py), samples s_j ..< s_end
-    uint32_t q = 0, s_i = 0, s_j = 0, s_end = 0, px = 0, py = 0;
+    // the lane's queue entry: stratum row s_i of pixel (px, py), samples
+    // s_j ..< s_end, partial-sum slot `slot`
+    uint32_t slot = 0, s_i = 0, s_j = 0, s_end = 0, px = 0, py = 0;
     bool need = true;
     bool in_path = false;
     Ray ray;
@@ -2023,7 +2025,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if (need) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                q = rank < avail ? old_next + rank : fresh + (rank - avail);
+                const uint32_t q = rank < avail ? old_next + rank : fresh + (rank - avail);
                 if (q >= F.queue_total) break;
                 need = false;
 #ifdef RT_WAVE_TRACE
@@ -2032,12 +2034,13 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_rays = n_rays;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                const uint32_t item = udiv_inv(q, F.inv_parts);
-                s_j = (q - item * F.parts) * F.part_len;
+                const uint32_t item = udiv_inv(q, F.inv_parts), part = q - item * F.parts;
+                s_j = part * F.part_len;
                 s_end = min(F.S, s_j + F.part_len);
                 acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S);
                 s_i = item - pl * F.S;
+                slot = (s_i * F.parts + part) * (F.W * F.rows) + pl;
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 px = pl - prow * F.W;
                 py = F.row_offset + prow * F.row_stride;
@@ -2103,7 +2106,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pst[0 * RT_BLOCK] = beta.x, pst[1 * RT_BLOCK] = beta.y, pst[2 * RT_BLOCK] = beta.z;
                 pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
                 pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
-                *pit = make_uint4(q, s_i | (s_end << 16), s_j, px | (py << 16));
+                *pit = make_uint4(slot, s_i | (s_end << 16), s_j, px | (py << 16));
                 if constexpr (PARK_RAY) {
                     pst[9 * RT_BLOCK] = ray.o.x, pst[10 * RT_BLOCK] = ray.o.y, pst[11 * RT_BLOCK] = ray.o.z;
                     pst[12 * RT_BLOCK] = ray.d.x, pst[13 * RT_BLOCK] = ray.d.y, pst[14 * RT_BLOCK] = ray.d.z;
@@ -2123,7 +2126,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
                 acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
                 const uint4 it = *pit;
-                q = it.x, s_i = it.y & 0xFFFFu, s_end = it.y >> 16, s_j = it.z, px = it.w & 0xFFFFu, py = it.w >> 16;
+                slot = it.x, s_i = it.y & 0xFFFFu, s_end = it.y >> 16, s_j = it.z, px = it.w & 0xFFFFu, py = it.w >> 16;
             }
         } else {
             const unsigned long long active = __ballot(true);
@@ -2161,7 +2164,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             in_path = false;
             ++s_j;
             if (s_j == s_end) {
-                double* dst = P->partial + (uint64_t)q * 3;
+                double* dst = P->partial + (uint64_t)slot * 3;
                 dst[0] = acc.x;
                 dst[1] = acc.y;
                 dst[2] = acc.z;
@@ -2285,7 +2288,8 @@ __device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
 }
 
 // Sums the S stratum rows of each pixel in s_i order -- a row = its `parts`
-// part sums added in part order -- * pixel_sample_scale,
+// part sums added in part order; slot (s_i * parts + part) * npix + pixel,
+// so a wave's loads are coalesced -- * pixel_sample_scale,
 // to linear f32 (camera.rs:193), and -- when srgb is given -- the pixel's
 // to_rgb bytes from the f64 sum, as the reference converts its f64 color.
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
@@ -2293,15 +2297,16 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
                                                        uint8_t* __restrict__ srgb, int toon) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
-    const double* src = partial + (uint64_t)p * S * parts * 3;
+    const double* src = partial + (uint64_t)p * 3;
+    const uint64_t step = (uint64_t)npix * 3;
     double r = 0.0, g = 0.0, b = 0.0;
     for (uint32_t k = 0; k < S; ++k) {
-        const double* row = src + k * parts * 3;
+        const double* row = src + (uint64_t)k * parts * step;
         double rr = row[0], rg = row[1], rb = row[2];
         for (uint32_t j = 1; j < parts; ++j) {
-            rr += row[j * 3 + 0];
-            rg += row[j * 3 + 1];
-            rb += row[j * 3 + 2];
+            rr += row[j * step + 0];
+            rg += row[j * step + 1];
+            rb += row[j * step + 2];
         }
         r += rr;
         g += rg;

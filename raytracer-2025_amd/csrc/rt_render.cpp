@@ -877,28 +877,25 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
     (void)hipSetDevice(d->device);
     hipError_t e = hipStreamSynchronize(d->last_stream);
     if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
-    if (d->parts <= 1) {
-        if (n && (e = hipMemcpy(out, d->partial, n * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy partials");
-        return RT_OK;
-    }
-    // rows traced in parts: a row's sum = its part sums added in part order,
-    // as rt_reduce_kernel adds them
-    std::vector<double> parts;
+    // device slots: (s_i * parts + part) * pixels + pixel (rtk::Frame); a
+    // row's sum = its part sums added in part order, as rt_reduce_kernel adds
+    std::vector<double> buf;
     try {
-        parts.resize(n * d->parts);
+        buf.resize(n * d->parts);
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }
-    if ((e = hipMemcpy(parts.data(), d->partial, parts.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
+    if (n && (e = hipMemcpy(buf.data(), d->partial, buf.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "hipMemcpy partials");
-    for (uint64_t row = 0; row < n / 3; ++row)
-        for (int c = 0; c < 3; ++c) {
-            const double* src = parts.data() + row * d->parts * 3 + c;
-            double sum = src[0];
-            for (uint32_t j = 1; j < d->parts; ++j) sum += src[j * 3];
-            out[row * 3 + c] = sum;
-        }
+    const uint64_t npix = (uint64_t)d->W * d->rows;
+    for (uint64_t pix = 0; pix < npix; ++pix)
+        for (uint32_t si = 0; si < d->S; ++si)
+            for (int c = 0; c < 3; ++c) {
+                const double* src = buf.data() + ((uint64_t)si * d->parts * npix + pix) * 3 + c;
+                double sum = src[0];
+                for (uint32_t j = 1; j < d->parts; ++j) sum += src[j * npix * 3];
+                out[(pix * d->S + si) * 3 + c] = sum;
+            }
     return RT_OK;
 }
 
