@@ -65,8 +65,8 @@ __device__ unsigned long long g_diag[16];
 #ifdef RT_WAVE_TRACE
 // trace build: per lane of the grid, {start, end (s_memrealtime, 100 MHz),
 // queue entries taken, rays traced, time / queue entry / rays so far at the
-// lane's last refill} (scripts/lane_trace.py)
-constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 8;
+// lane's last refill, s_memtime ticks from start to end} (scripts/lane_trace.py)
+constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 10;
 __device__ unsigned long long g_lane_trace[RT_TRACE_LANES * RT_TRACE_W];
 #endif
 
@@ -89,10 +89,18 @@ struct Frame {
     // pixel whose paths bounce 40 times inside a glass sphere is ~10 ms of one
     // wave (scripts/lane_trace.py): parts keep the last entries short.
     uint32_t parts, part_len, queue_total;
+    // The launch's last parts (entries >= head_entries) go out one sample per
+    // entry: entry head_entries + t is sample t % part_len of part
+    // head_entries + t / part_len (none past the part's end), its value
+    // written to slot tail_slot + t; rt_tail_combine_kernel adds a part's
+    // samples in order -- the bits the part's lane sum would have (0 + v0 +
+    // v1 + ...), so the split never shows in the image.
+    uint32_t head_entries, tail_slot;
+    uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
-    // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
-    // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
-    double inv_parts, inv_S, inv_W;
+    // 1/parts, 1/S, 1/W, 1/part_len rounded up (udiv_inv), and 1/(waves of
+    // the grid x RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
+    double inv_parts, inv_S, inv_W, inv_len;
     float inv_guide;
     uint32_t defocus;
     double recip_sqrt_spp, pixel_sample_scale;
@@ -1095,10 +1103,17 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #define RT_DEFER_THRESH 48  // lanes with a queued sphere that trigger a sphere round
 #endif
 #ifndef RT_DEFER_REL
-// ... or 3/4 of the lanes still in the walk, when fewer than 64 are: a wave
-// thinned out at the end of a launch tests its queued spheres instead of
-// walking on unbounded until none of its lanes can
+// ... or 3/4 of the lanes still in the walk, when fewer than 64 are; and any
+// one of them when at most RT_DEFER_THIN are: a wave thinned out at the end
+// of a launch tests its queued spheres at once.  A ray trapped in a glass
+// sphere by total internal reflection bounces to max_depth, and each bounce
+// queues the sphere it starts on (its origin is on the surface: the filter
+// can bound nothing); without the round its walk went on along the whole
+// line through the scene -- 70 us per bounce in the lane trace's last waves.
 #define RT_DEFER_REL 1
+#endif
+#ifndef RT_DEFER_THIN
+#define RT_DEFER_THIN 16
 #endif
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
@@ -1248,7 +1263,8 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const unsigned long long mp0 = __ballot(pn > 0);
 #if RT_DEFER_REL
     const uint32_t in_walk = (uint32_t)__popcll(__ballot(true));
-    const uint32_t thresh = min((uint32_t)RT_DEFER_THRESH, (in_walk * 3u + 3u) / 4u);
+    const uint32_t thresh =
+        in_walk <= RT_DEFER_THIN ? 1u : min((uint32_t)RT_DEFER_THRESH, (in_walk * 3u + 3u) / 4u);
 #else
     constexpr uint32_t thresh = RT_DEFER_THRESH;
 #endif
@@ -1975,14 +1991,24 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     uint32_t vertex = 0;
     uint32_t n_rays = 0, n_panics = 0;
 
-    uint32_t pool_next = 0, pool_end = 0;  // wave-uniform: items this wave holds
+    // wave-uniform: the queue entries this wave holds.  Wave w starts with the
+    // 64 entries [64 w, 64 w + 64) -- no atomic at launch: 4096 waves taking
+    // their first chunk from one counter at once waited up to 2.9 ms for it
+    // (scripts/lone_wave.py) -- and the counter hands out entries from
+    // Frame::static_entries on.  `dry`: an atomic of this wave has passed the
+    // end of the queue, so none will hand out entries any more -- lanes that
+    // need one leave without another atomic (the drain's waves waited ~70 us
+    // a round on the counter the whole grid hammered).
+    uint32_t pool_next = (blockIdx.x * (BLK / 64) + threadIdx.x / 64) * 64u, pool_end = pool_next + 64u;
+    bool dry = false;
     Diag dg;
     Trav<TIER> T;
     bool walking = false;
 #ifdef RT_WAVE_TRACE
     const uint32_t trace_lane = blockIdx.x * BLK + threadIdx.x;
     const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t trace_items = 0, trace_q = 0, trace_rays = 0;
+    const unsigned long long trace_c0 = __builtin_amdgcn_s_memtime();
+    uint32_t trace_items = 0, trace_q = 0, trace_rays = 0, trace_steps = 0, trace_steps_q = 0;
     unsigned long long trace_tq = trace_t0;
 #endif
     for (;;) {
@@ -2011,9 +2037,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             }
 #endif
             if (avail < n) {
-                const uint32_t leader = __ffsll((long long)mask) - 1;
-                if (lane == leader) fresh = atomicAdd(queue, chunk);
-                fresh = __shfl(fresh, leader);
+                if (!dry) {
+                    const uint32_t leader = __ffsll((long long)mask) - 1;
+                    if (lane == leader) fresh = atomicAdd(queue, chunk);
+                    fresh = __shfl(fresh, leader) + F.static_entries;
+                    dry = fresh + chunk >= F.queue_total;
+                } else {
+                    fresh = F.queue_total;  // past the end: the needy lanes leave
+                }
             }
             const uint32_t old_next = pool_next;
             if (avail < n) {
@@ -2032,21 +2063,36 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 ++trace_items;
                 trace_q = q;
                 trace_rays = n_rays;
+                trace_steps_q = trace_steps;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                const uint32_t item = udiv_inv(q, F.inv_parts), part = q - item * F.parts;
+                uint32_t qe = q, k = 0;  // the part, and the sample in it of a tail entry
+                const bool tail = q >= F.head_entries;
+                if (tail) {
+                    const uint32_t t = q - F.head_entries, tp = udiv_inv(t, F.inv_len);
+                    k = t - tp * F.part_len;
+                    qe = F.head_entries + tp;
+                }
+                const uint32_t item = udiv_inv(qe, F.inv_parts), part = qe - item * F.parts;
                 s_j = part * F.part_len;
                 s_end = min(F.S, s_j + F.part_len);
                 acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S);
                 s_i = item - pl * F.S;
                 slot = (s_i * F.parts + part) * (F.W * F.rows) + pl;
+                if (tail) {
+                    s_j += k;
+                    need = s_j >= s_end;  // past a short part's end: nothing to trace
+                    s_end = s_j + 1;
+                    slot = F.tail_slot + (q - F.head_entries);
+                }
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 px = pl - prow * F.W;
                 py = F.row_offset + prow * F.row_stride;
                 rng.pixel = py * F.W + px;
             }
         }
+        if (need) continue;  // an empty tail entry: take the next one
         if (!in_path) {
             // ---- Camera::get_ray (camera.rs:247-273), vertex 0
             rng.sample = s_i * F.S + s_j;
@@ -2113,7 +2159,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                     pst[15 * RT_BLOCK] = ray.time;
                 }
             }
+#ifdef RT_WAVE_TRACE
+            while (walking) walking = step(), ++trace_steps;
+#else
             while (walking) walking = step();
+#endif
             RT_DIAG_ONLY(const unsigned long long t_m0 = __builtin_amdgcn_s_memtime();)
             if constexpr (PARK_RAY)
                 media_phase<TIER>(S, RayLds{pst + 9 * RT_BLOCK}, T, stk, rng, med);
@@ -2201,11 +2251,23 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         t[4] = trace_tq;
         t[5] = trace_q;
         t[6] = trace_rays;
-        t[7] = 0;
+        t[7] = __builtin_amdgcn_s_memtime() - trace_c0;  // shader clocks over the lane's life
+        t[8] = trace_steps;  // walk steps (wave iterations the lane walked in)
+        t[9] = trace_steps_q;  // ... at its last refill
     }
 #endif
-    atomicAdd(&P->stats[0], (unsigned long long)n_rays);
-    if (n_panics) atomicAdd(&P->stats[1], (unsigned long long)n_panics);
+    // one atomic per wave, not per lane: 262 144 adds to one address at the
+    // end of every launch
+    uint32_t rays_w = n_rays, panics_w = n_panics;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        rays_w += __shfl_xor(rays_w, o);
+        panics_w += __shfl_xor(panics_w, o);
+    }
+    if (lane == 0) {
+        atomicAdd(&P->stats[0], (unsigned long long)rays_w);
+        if (panics_w) atomicAdd(&P->stats[1], (unsigned long long)panics_w);
+    }
 }
 
 }  // namespace rtk
@@ -2322,6 +2384,24 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     }
 }
 
+// The launch's tail parts, traced one sample per entry (Frame::head_entries):
+// each part's sum = 0 + its samples in order, into the part's slot.  One
+// thread per (part, channel).
+__global__ void __launch_bounds__(256) rt_tail_combine_kernel(const double* __restrict__ partial_in,
+                                                              double* __restrict__ partial, Frame F,
+                                                              uint32_t tail_parts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= tail_parts * 3) return;
+    const uint32_t tp = i / 3, c = i - tp * 3;
+    const uint32_t qe = F.head_entries + tp, item = qe / F.parts, part = qe - item * F.parts;
+    const uint32_t pl = item / F.S, s_i = item - pl * F.S;
+    const uint32_t n = min(F.S, (part + 1) * F.part_len) - part * F.part_len;
+    const double* src = partial_in + ((uint64_t)F.tail_slot + (uint64_t)tp * F.part_len) * 3 + c;
+    double sum = 0.0;
+    for (uint32_t k = 0; k < n; ++k) sum += src[k * 3];
+    partial[((uint64_t)(s_i * F.parts + part) * (F.W * F.rows) + pl) * 3 + c] = sum;
+}
+
 // to_rgb of a linear f32 framebuffer already on the device (e.g. the gathered
 // multi-GPU frame).
 __global__ void __launch_bounds__(256) rt_to_rgb_kernel(const float* __restrict__ lin, uint8_t* __restrict__ srgb,
@@ -2384,12 +2464,18 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.total_items = fd->W * fd->rows * fd->S;
     F.parts = fd->parts > 1 ? fd->parts : 1u;  // the host's rtk_row_parts: no part empty
     F.part_len = (fd->S + F.parts - 1) / F.parts;
-    F.queue_total = F.total_items * F.parts;
+    const uint32_t entries = F.total_items * F.parts;
+    const uint32_t tail_parts = F.part_len > 1 ? min(fd->tail_parts, entries) : 0u;
+    F.head_entries = entries - tail_parts;
+    F.tail_slot = entries;  // tail sample slots follow the part slots
+    F.queue_total = F.head_entries + tail_parts * F.part_len;
+    F.static_entries = (uint32_t)grid * (uint32_t)rtk_block_threads(tier);
     F.chunk_min = fd->chunk_min;
     auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
     F.inv_parts = inv_up(F.parts);
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
+    F.inv_len = inv_up(F.part_len);
     F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
@@ -2417,6 +2503,9 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
                                       : rtk_launch_path_4(grid, stream, Pd);
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
+    if (tail_parts > 0)
+        hipLaunchKernelGGL(rtk::rt_tail_combine_kernel, dim3((tail_parts * 3 + 255) / 256), dim3(256), 0, stream,
+                           partial, partial, F, tail_parts);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
                        F.parts, fd->pixel_sample_scale, out, srgb, toon);

@@ -34,13 +34,13 @@ def main():
     world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
     cam.render(world, lights, seed=1, want_srgb=False)
     n = 1 << 19
-    buf = (ctypes.c_ulonglong * (n * 8))()
+    buf = (ctypes.c_ulonglong * (n * 10))()
     for stride in strides:
         ctypes.memset(buf, 0, ctypes.sizeof(buf))
         torch.cuda.synchronize()
         _, _, st = cam.render(world, lights, seed=1, row_stride=stride, want_srgb=False)
         assert lib.rt_lane_trace(buf, n) == 0
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 8).astype(np.int64)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
         a = a[a[:, 1] > 0]
         t0, t1 = a[:, 0].min(), a[:, 1].max()
         span = (t1 - t0) / 100.0  # 100 MHz -> us
@@ -66,6 +66,30 @@ def main():
         rec["last_lanes"] = [{"end_ms": round((a[i, 1] - t0) / 1e5, 3), "last_entry_ms": round((a[i, 4] - t0) / 1e5, 3),
                               "q": int(a[i, 5]), "pixel": int(a[i, 5] // S), "rays_after": int(a[i, 3] - a[i, 6]),
                               "entries": int(a[i, 2])} for i in last]
+        # the slowest waves: rounds (rays) their busiest lane traced after the
+        # wave's queue ran dry, and the rate
+        idx = np.arange(len(a))
+        wend = {}
+        for w in np.unique(idx // 64):
+            sl = slice(w * 64, w * 64 + 64)
+            wend[int(w)] = int(a[sl, 1].max())
+        slow = sorted(wend, key=wend.get)[-5:][::-1]
+        rec["slow_waves"] = []
+        for w in slow:
+            sl = slice(w * 64, w * 64 + 64)
+            t_dry = a[sl, 4].max()
+            ra = a[sl, 3] - a[sl, 6]
+            rec["slow_waves"].append({"end_ms": round((wend[w] - t0) / 1e5, 3),
+                                      "last_refill_ms": round((t_dry - t0) / 1e5, 3),
+                                      "max_rays_after_last_entry": int(ra.max()),
+                                      "lanes_rays_after_gt10": int((ra > 10).sum()),
+                                      "us_per_round": round((wend[w] - t_dry) / 100.0 / max(1, int(ra.max())), 2),
+                                      "steps_after_busiest": int((a[sl, 8] - a[sl, 9])[np.argmax(ra)]),
+                                      "steps_per_ray_busiest": round(float((a[sl, 8] - a[sl, 9])[np.argmax(ra)]) / max(1, int(ra.max())), 1),
+                                      "memtime_mhz": round(float(a[sl, 7].max()) / ((wend[w] - a[sl, 0].min()) / 100.0), 1)})
+        life = (a[:, 1] - a[:, 0]) / 100.0
+        rec["steps_per_ray_mean"] = round(float(a[:, 8].sum()) / float(a[:, 3].sum()), 2)
+        rec["memtime_mhz_median"] = round(float(np.median(a[:, 7] / np.maximum(life, 1e-9))), 1)
         rec["last_entry_ms_pct"] = {p: round(float(np.percentile((a[:, 4] - t0) / 1e5, p)), 3) for p in (50, 99, 100)}
         print(json.dumps(rec), flush=True)
 

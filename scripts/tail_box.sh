@@ -1,7 +1,7 @@
 #!/bin/bash
 # gpurun: GPU parity tests, then the shard-scaling rehearsal
 # (scripts/shard_scaling.py) under queue settings name:RT_PART_SAMPLES:
-# RT_CHUNK_MIN (TAIL_CFGS).
+# RT_CHUNK_MIN:RT_TAIL_SAMPLES (TAIL_CFGS).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
@@ -12,8 +12,8 @@ if [ "${TAIL_TESTS:-1}" = 1 ]; then
   tail -2 $OUT/pytest.log
 fi
 for cfg in ${TAIL_CFGS:-old:0:64 d:6:0}; do
-  IFS=: read name samples cmin <<< "$cfg"
-  RT_PART_SAMPLES=$samples RT_CHUNK_MIN=$cmin timeout -k 10 200 python3 scripts/shard_scaling.py ${TAIL_WL:-c2} ${TAIL_SPP:-512} 3 > $OUT/${TAIL_WL:-c2}_$name.jsonl 2> $OUT/${TAIL_WL:-c2}_$name.err || { echo "shard $name failed"; tail -5 $OUT/${TAIL_WL:-c2}_$name.err; exit 1; }
+  IFS=: read name samples cmin tail <<< "$cfg"
+  RT_PART_SAMPLES=$samples RT_CHUNK_MIN=$cmin RT_TAIL_SAMPLES=${tail:-48} timeout -k 10 200 python3 scripts/shard_scaling.py ${TAIL_WL:-c2} ${TAIL_SPP:-512} 3 > $OUT/${TAIL_WL:-c2}_$name.jsonl 2> $OUT/${TAIL_WL:-c2}_$name.err || { echo "shard $name failed"; tail -5 $OUT/${TAIL_WL:-c2}_$name.err; exit 1; }
   echo "$name: $(tail -1 $OUT/${TAIL_WL:-c2}_$name.jsonl | python3 -c 'import json,sys; d=json.load(sys.stdin); print("full_ms", round(d["full_ms"],2), "eff8", d["eff8_worst_rank"], [ (r["n"], r["kernel_ms"]) for r in d["runs"] if r["rank"]==0])')"
 done
 echo tail-box-done

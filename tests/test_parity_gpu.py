@@ -187,6 +187,31 @@ def test_shard_rows_equal_full_frame(gpu, rt, scenes):
         np.testing.assert_array_equal(part, full[off::stride])
 
 
+@pytest.mark.parametrize("spp", [64, 484])
+def test_queue_split_is_bit_exact(gpu, rt, scenes, monkeypatch, spp):
+    """The work queue's splits never show in the result: stratum rows in parts
+    (RT_PART_SAMPLES) are a function of the frame, and a part traced one
+    sample per entry at the end of a launch (RT_TAIL_SAMPLES) is summed as
+    its lane would have summed it.  Images and (pixel, s_i) sums are
+    bit-equal whether no part, some parts or every part goes out per sample,
+    and for every row shard."""
+    scene = rt.Scene(gpu)
+    world, lights, cam = scenes.random_spheres(scene, 96, spp)
+    runs = []
+    for tail in ("0", "1", "8", "100000"):
+        monkeypatch.setenv("RT_TAIL_SAMPLES", tail)
+        lin, _, st = cam.render(world, lights, seed=5, want_srgb=False)
+        runs.append((lin, gpu_partials(gpu, scene, cam, lin.shape[0])))
+        assert st.samples == 96 * 54 * cam.sqrt_spp ** 2
+    for lin, part in runs[1:]:
+        np.testing.assert_array_equal(lin, runs[0][0])
+        np.testing.assert_array_equal(part, runs[0][1])
+    monkeypatch.setenv("RT_TAIL_SAMPLES", "8")
+    for off, stride in ((1, 3), (0, 8)):
+        shard, _, _ = cam.render(world, lights, seed=5, row_offset=off, row_stride=stride, want_srgb=False)
+        np.testing.assert_array_equal(shard, runs[0][0][off::stride])
+
+
 def test_deterministic_and_seeded(gpu, rt, scenes):
     scene = rt.Scene(gpu)
     world, lights, cam = scenes.random_spheres(scene, 64, 9)
