@@ -80,10 +80,7 @@ struct rtk_frame_desc {
     // samples (rtk::Frame::parts; rtk_row_parts), summed in part order
     uint32_t parts;
     uint32_t chunk_min;  // smallest guided chunk of queue entries (0: what the wave needs)
-    // the launch's last tail_parts parts go out one sample per queue entry
-    // (rtk::Frame::head_entries); their samples need tail_parts * ceil(S /
-    // parts) slots after the W * rows * S * parts part slots of `partial`
-    uint32_t tail_parts, pad3;
+
     double recip_sqrt_spp, pixel_sample_scale;
     double center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3];
     void* ev_start;  // hipEvent_t recorded around the path kernel (or NULL)

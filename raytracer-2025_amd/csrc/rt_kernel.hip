@@ -89,18 +89,11 @@ struct Frame {
     // pixel whose paths bounce 40 times inside a glass sphere is ~10 ms of one
     // wave (scripts/lane_trace.py): parts keep the last entries short.
     uint32_t parts, part_len, queue_total;
-    // The launch's last parts (entries >= head_entries) go out one sample per
-    // entry: entry head_entries + t is sample t % part_len of part
-    // head_entries + t / part_len (none past the part's end), its value
-    // written to slot tail_slot + t; rt_tail_combine_kernel adds a part's
-    // samples in order -- the bits the part's lane sum would have (0 + v0 +
-    // v1 + ...), so the split never shows in the image.
-    uint32_t head_entries, tail_slot;
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
-    // 1/parts, 1/S, 1/W, 1/part_len rounded up (udiv_inv), and 1/(waves of
-    // the grid x RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
-    double inv_parts, inv_S, inv_W, inv_len;
+    // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
+    // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
+    double inv_parts, inv_S, inv_W;
     float inv_guide;
     uint32_t defocus;
     double recip_sqrt_spp, pixel_sample_scale;
@@ -1981,9 +1974,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     Rng rng;
     rng.k0 = F.key0;
     rng.k1 = F.key1;
-    // the lane's queue entry: stratum row s_i of pixel (px, py), samples
-    // s_j ..< s_end, partial-sum slot `slot`
-    uint32_t slot = 0, s_i = 0, s_j = 0, s_end = 0, px = 0, py = 0;
+    // the lane's queue entry: stratum row s_i of pixel rng.pixel (= py * W +
+    // px), samples s_j ..< s_end (sie = s_i | s_end << 16: S < 2^16),
+    // partial-sum slot `slot` -- few registers across the path loop
+    uint32_t slot = 0, s_j = 0, sie = 0;
     bool need = true;
     bool in_path = false;
     Ray ray;
@@ -2066,35 +2060,19 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_steps_q = trace_steps;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                uint32_t qe = q, k = 0;  // the part, and the sample in it of a tail entry
-                const bool tail = q >= F.head_entries;
-                if (tail) {
-                    const uint32_t t = q - F.head_entries, tp = udiv_inv(t, F.inv_len);
-                    k = t - tp * F.part_len;
-                    qe = F.head_entries + tp;
-                }
-                const uint32_t item = udiv_inv(qe, F.inv_parts), part = qe - item * F.parts;
+                const uint32_t item = udiv_inv(q, F.inv_parts), part = q - item * F.parts;
                 s_j = part * F.part_len;
-                s_end = min(F.S, s_j + F.part_len);
                 acc = d3(0, 0, 0);
-                const uint32_t pl = udiv_inv(item, F.inv_S);
-                s_i = item - pl * F.S;
+                const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
+                sie = s_i | (min(F.S, s_j + F.part_len) << 16);
                 slot = (s_i * F.parts + part) * (F.W * F.rows) + pl;
-                if (tail) {
-                    s_j += k;
-                    need = s_j >= s_end;  // past a short part's end: nothing to trace
-                    s_end = s_j + 1;
-                    slot = F.tail_slot + (q - F.head_entries);
-                }
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
-                px = pl - prow * F.W;
-                py = F.row_offset + prow * F.row_stride;
-                rng.pixel = py * F.W + px;
+                rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
             }
         }
-        if (need) continue;  // an empty tail entry: take the next one
         if (!in_path) {
             // ---- Camera::get_ray (camera.rs:247-273), vertex 0
+            const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
             rng.sample = s_i * F.S + s_j;
             rng.begin(0);
             uint32_t ovf = 0;
@@ -2152,7 +2130,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pst[0 * RT_BLOCK] = beta.x, pst[1 * RT_BLOCK] = beta.y, pst[2 * RT_BLOCK] = beta.z;
                 pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
                 pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
-                *pit = make_uint4(slot, s_i | (s_end << 16), s_j, px | (py << 16));
+                *pit = make_uint4(slot, sie, s_j, 0u);
                 if constexpr (PARK_RAY) {
                     pst[9 * RT_BLOCK] = ray.o.x, pst[10 * RT_BLOCK] = ray.o.y, pst[11 * RT_BLOCK] = ray.o.z;
                     pst[12 * RT_BLOCK] = ray.d.x, pst[13 * RT_BLOCK] = ray.d.y, pst[14 * RT_BLOCK] = ray.d.z;
@@ -2176,7 +2154,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
                 acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
                 const uint4 it = *pit;
-                slot = it.x, s_i = it.y & 0xFFFFu, s_end = it.y >> 16, s_j = it.z, px = it.w & 0xFFFFu, py = it.w >> 16;
+                slot = it.x, sie = it.y, s_j = it.z;
             }
         } else {
             const unsigned long long active = __ballot(true);
@@ -2213,7 +2191,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             acc = acc + L;
             in_path = false;
             ++s_j;
-            if (s_j == s_end) {
+            if (s_j == (sie >> 16)) {
                 double* dst = P->partial + (uint64_t)slot * 3;
                 dst[0] = acc.x;
                 dst[1] = acc.y;
@@ -2384,24 +2362,6 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     }
 }
 
-// The launch's tail parts, traced one sample per entry (Frame::head_entries):
-// each part's sum = 0 + its samples in order, into the part's slot.  One
-// thread per (part, channel).
-__global__ void __launch_bounds__(256) rt_tail_combine_kernel(const double* __restrict__ partial_in,
-                                                              double* __restrict__ partial, Frame F,
-                                                              uint32_t tail_parts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= tail_parts * 3) return;
-    const uint32_t tp = i / 3, c = i - tp * 3;
-    const uint32_t qe = F.head_entries + tp, item = qe / F.parts, part = qe - item * F.parts;
-    const uint32_t pl = item / F.S, s_i = item - pl * F.S;
-    const uint32_t n = min(F.S, (part + 1) * F.part_len) - part * F.part_len;
-    const double* src = partial_in + ((uint64_t)F.tail_slot + (uint64_t)tp * F.part_len) * 3 + c;
-    double sum = 0.0;
-    for (uint32_t k = 0; k < n; ++k) sum += src[k * 3];
-    partial[((uint64_t)(s_i * F.parts + part) * (F.W * F.rows) + pl) * 3 + c] = sum;
-}
-
 // to_rgb of a linear f32 framebuffer already on the device (e.g. the gathered
 // multi-GPU frame).
 __global__ void __launch_bounds__(256) rt_to_rgb_kernel(const float* __restrict__ lin, uint8_t* __restrict__ srgb,
@@ -2464,18 +2424,13 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.total_items = fd->W * fd->rows * fd->S;
     F.parts = fd->parts > 1 ? fd->parts : 1u;  // the host's rtk_row_parts: no part empty
     F.part_len = (fd->S + F.parts - 1) / F.parts;
-    const uint32_t entries = F.total_items * F.parts;
-    const uint32_t tail_parts = F.part_len > 1 ? min(fd->tail_parts, entries) : 0u;
-    F.head_entries = entries - tail_parts;
-    F.tail_slot = entries;  // tail sample slots follow the part slots
-    F.queue_total = F.head_entries + tail_parts * F.part_len;
+    F.queue_total = F.total_items * F.parts;
     F.static_entries = (uint32_t)grid * (uint32_t)rtk_block_threads(tier);
     F.chunk_min = fd->chunk_min;
     auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
     F.inv_parts = inv_up(F.parts);
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
-    F.inv_len = inv_up(F.part_len);
     F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
@@ -2503,9 +2458,6 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
                                       : rtk_launch_path_4(grid, stream, Pd);
     if (e != hipSuccess) return e;
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
-    if (tail_parts > 0)
-        hipLaunchKernelGGL(rtk::rt_tail_combine_kernel, dim3((tail_parts * 3 + 255) / 256), dim3(256), 0, stream,
-                           partial, partial, F, tail_parts);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
                        F.parts, fd->pixel_sample_scale, out, srgb, toon);

@@ -435,6 +435,7 @@ static int32_t init_frame(const rt_camera* c, uint64_t seed, uint32_t row_offset
     f.recip_sqrt_spp = 1.0 / (double)f.S;
     if ((uint64_t)W * f.rows * f.S >= 0xFFF00000ull) return set_error(RT_EINVAL, "frame too large for one launch");
     if (W >= (1u << 20)) return set_error(RT_EINVAL, "image_width must be below 2^20");
+    if (f.S >= (1u << 16)) return set_error(RT_EINVAL, "samples_per_pixel must be below 2^32");
     V3 from(c->look_from), at(c->look_at), up(c->vec_up);
     double theta = c->vertical_fov_in_degrees * (PI / 180.0);
     double h = std::tan(theta / 2.0);
@@ -529,18 +530,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     f.parts = rtk_row_parts(f.W, rt_camera_image_height(cam), f.S, env_u32("RT_PART_SAMPLES", 4),
                             (uint64_t)env_u32("RT_PART_BUDGET_MB", 8192) << 20);
     f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
-    // ... and the launch's last parts one sample per entry: about
-    // RT_TAIL_SAMPLES (48) samples for every lane of the grid, so that the
-    // longest entries in flight when the queue runs dry are single paths
-    const uint32_t part_len = (f.S + f.parts - 1) / f.parts;
-    const uint64_t entries = (uint64_t)f.W * f.rows * f.S * f.parts;
-    const uint64_t lanes = (uint64_t)d->grid[d->tier] * rtk_block_threads(d->tier);
-    f.tail_parts = part_len > 1 ? (uint32_t)std::min<uint64_t>(
-                                      entries, lanes * env_u32("RT_TAIL_SAMPLES", 48) / part_len)
-                                : 0;
-    if (entries + (uint64_t)f.tail_parts * part_len >= 0xFFF00000ull) f.tail_parts = 0;
-    if ((rc = grow((void**)&d->partial, d->partial_bytes,
-                   (size_t)(entries + (uint64_t)f.tail_parts * part_len) * 3 * sizeof(double),
+    if ((rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * f.parts * 3 * sizeof(double),
                    "hipMalloc partial sums")) != RT_OK)
         return fail(rc);
     if (!p.out &&
