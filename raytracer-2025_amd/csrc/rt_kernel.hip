@@ -1110,6 +1110,9 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #endif
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
+#ifndef RT_SLOT_BALLOT
+#define RT_SLOT_BALLOT 1
+#endif
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
 // lane's LDS queue, pq[k * RT_BLOCK_BASIC], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
@@ -1138,6 +1141,35 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
     bool sph[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) sph[i] = ref_kind(R[i]) == K_SPHERE;
+    constexpr float INF = __builtin_huge_valf();
+    float key[4];
+    uint32_t ref[4];
+#if RT_SLOT_BALLOT
+    // per slot, the filter / slab only when some lane has a sphere / a box
+    // there: the flatten puts a node's spheres in its low slots and its empty
+    // slots last (rth::bvh4_convert), and most leaf-level nodes hold 2-3 spheres
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (__ballot(sph[i])) {
+            if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
+                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_index(R[i]);
+                ++pn;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool box = R[i] != REF_NONE && !sph[i];
+        key[i] = INF;
+        ref[i] = R[i];
+        if (__ballot(box)) {
+            const float lo[3] = {LX[i], LY[i], LZ[i]}, hi[3] = {HX[i], HY[i], HZ[i]};
+            float e;
+            const bool h = slab_f(lo, hi, rf, tmin_f, c_f, e) && box;
+            key[i] = h ? e : INF;
+        }
+    }
+#else
     if (__ballot(sph[0] || sph[1] || sph[2] || sph[3])) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1147,9 +1179,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
             }
         }
     }
-    constexpr float INF = __builtin_huge_valf();
-    float key[4];
-    uint32_t ref[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const float lo[3] = {LX[i], LY[i], LZ[i]}, hi[3] = {HX[i], HY[i], HZ[i]};
@@ -1158,6 +1187,7 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
         key[i] = h ? e : INF;
         ref[i] = R[i];
     }
+#endif
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];

@@ -1279,6 +1279,10 @@ void rt_scene_destroy(rt_scene* s) {
 namespace rth {
 }  // namespace rth
 
+#ifndef RT_BVH4_SPHERES_FIRST
+#define RT_BVH4_SPHERES_FIRST 1
+#endif
+
 namespace rth {
 // Collapses the two-box BVHs of a world into 4-wide nodes: starting from a
 // node's two children, the inner child with the largest box (surface area) is
@@ -1339,6 +1343,15 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
             ch.erase(ch.begin() + best);
             ch.insert(ch.begin() + best, sub.begin(), sub.end());
         }
+#if RT_BVH4_SPHERES_FIRST
+        // basic tier: sphere children in the low slots, boxes after them, empty
+        // slots last -- a wave tests a slot's filter / slab only when one of its
+        // lanes has that kind there (rt_kernel.hip visit4_rows); most leaf-level
+        // nodes hold 2 or 3 spheres
+        if (filter_spheres)
+            std::stable_partition(ch.begin(), ch.end(),
+                                  [](const Child& c) { return rtk::ref_kind(c.ref) == rtk::K_SPHERE; });
+#endif
         const uint32_t at = (uint32_t)out.size();
         out.emplace_back();
         map[idx] = rtk::make_ref(rtk::K_BVH, at);
