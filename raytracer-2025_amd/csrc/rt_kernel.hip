@@ -1169,7 +1169,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
             key[i] = h ? e : INF;
         }
     }
-
 #else
     if (__ballot(sph[0] || sph[1] || sph[2] || sph[3])) {
 #pragma unroll
