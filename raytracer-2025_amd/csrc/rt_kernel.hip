@@ -2120,7 +2120,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             }
             ray.o = origin;
             ray.d = ps - origin;
-            ray.time = rng.next(ovf);
+            // the ray's time (vertex 0's last draw) is read only by moving
+            // spheres, which only the full tiers hold: the basic and mesh
+            // tiers skip its Philox block (no other draw depends on it)
+            ray.time = tier_full(TIER) ? rng.next(ovf) : 0.0;
             beta = d3(1, 1, 1);
             L = d3(0, 0, 0);
             vertex = 1;
