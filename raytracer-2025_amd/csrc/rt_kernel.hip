@@ -1919,6 +1919,14 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #ifndef RT_QUEUE_CHUNK
 #define RT_QUEUE_CHUNK 256  // most items a wave takes per queue atomic (>= 64)
 #endif
+#ifndef RT_QUEUE_CHUNK_MESH
+// the mesh tier's cap: its rounds are long (a dependent global load per walk
+// step) and a pool of 256 entries can outlive the queue by milliseconds, but
+// smaller caps cost the whole frame more in counter contention than they
+// save at the end (C4: 128 -> +2 % frame, 1/8 shard 30.0 -> 27.3 ms; 64 ->
+// +6 %, 27.2 ms)
+#define RT_QUEUE_CHUNK_MESH RT_QUEUE_CHUNK
+#endif
 #ifndef RT_QUEUE_GUIDE
 #define RT_QUEUE_GUIDE 8  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
 #endif
@@ -2057,7 +2065,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             {
                 const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
                 const uint32_t g = max((uint32_t)((float)left * F.inv_guide), F.chunk_min);
-                chunk = max(min(g, (uint32_t)RT_QUEUE_CHUNK), avail < n ? n - avail : 0u);
+                constexpr uint32_t CAP = TIER == TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK;
+                chunk = max(min(g, CAP), avail < n ? n - avail : 0u);
             }
 #endif
             if (avail < n) {
