@@ -84,10 +84,11 @@ struct Frame {
     // Work queue: entry q = part q % parts of stratum row q / parts (item =
     // launch pixel * S + s_i); a part traces part_len consecutive samples s_j
     // (the last part the rest) and writes their f64 sum to partial slot
-    // (s_i * parts + part) * pixels + pixel -- pixel-minor, so that the reduce
-    // reads coalesced -- and the reduce adds a row's parts in order.  A launch ends on its longest queue entries, and a whole row of a
-    // pixel whose paths bounce 40 times inside a glass sphere is ~10 ms of one
-    // wave (scripts/lane_trace.py): parts keep the last entries short.
+    // (s_i * parts + part) * pixels + pixel -- pixel-minor, so that the
+    // reduce reads coalesced -- and the reduce adds a row's parts in order.
+    // A launch ends on its longest queue entries, and a whole row of a pixel
+    // whose paths bounce 40 times inside a glass sphere is ~10 ms of one wave
+    // (scripts/lane_trace.py): parts keep the last entries short.
     uint32_t parts, part_len, queue_total;
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
@@ -1098,11 +1099,12 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #ifndef RT_DEFER_REL
 // ... or 3/4 of the lanes still in the walk, when fewer than 64 are; and any
 // one of them when at most RT_DEFER_THIN are: a wave thinned out at the end
-// of a launch tests its queued spheres at once.  A ray trapped in a glass
-// sphere by total internal reflection bounces to max_depth, and each bounce
-// queues the sphere it starts on (its origin is on the surface: the filter
-// can bound nothing); without the round its walk went on along the whole
-// line through the scene -- 70 us per bounce in the lane trace's last waves.
+// of a launch tests its queued spheres at once instead of walking on with an
+// unbounded walk (a ray trapped in a glass sphere queues the sphere it starts
+// on at every bounce: its origin is on the surface, so the filter can bound
+// nothing).  Measured within noise on the whole frame and on the 1/8 shard:
+// the slow last waves of the lane trace were the exit atomics' (the kernel's
+// end), not this.
 #define RT_DEFER_REL 1
 #endif
 #ifndef RT_DEFER_THIN
