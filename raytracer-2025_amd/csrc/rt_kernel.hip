@@ -1929,6 +1929,16 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 // +6 %, 27.2 ms)
 #define RT_QUEUE_CHUNK_MESH RT_QUEUE_CHUNK
 #endif
+#ifndef RT_QUEUE_CHUNK_BASIC
+// the basic tier (C2): twice the cap with chunks shrinking twice as fast
+// (guide 16): half the counter's atomics early, smaller pools late -- C2
+// 186.3 -> 184.8 ms frame, 1/8 shard 24.8 -> 24.3 ms (A/B, 2 interleaved
+// reps; cap 512 at guide 8: frame -1.1 % but the shard +11 %)
+#define RT_QUEUE_CHUNK_BASIC 512
+#endif
+#ifndef RT_QUEUE_GUIDE_BASIC
+#define RT_QUEUE_GUIDE_BASIC 16
+#endif
 #ifndef RT_QUEUE_GUIDE
 #define RT_QUEUE_GUIDE 8  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
 #endif
@@ -2067,7 +2077,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             {
                 const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
                 const uint32_t g = max((uint32_t)((float)left * F.inv_guide), F.chunk_min);
-                constexpr uint32_t CAP = TIER == TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK;
+                constexpr uint32_t CAP = TIER == TIER_MESH    ? RT_QUEUE_CHUNK_MESH
+                                         : TIER == TIER_BASIC ? RT_QUEUE_CHUNK_BASIC
+                                                              : RT_QUEUE_CHUNK;
                 chunk = max(min(g, CAP), avail < n ? n - avail : 0u);
             }
 #endif
@@ -2475,7 +2487,8 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.inv_parts = inv_up(F.parts);
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
-    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
+    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) *
+                                 (tier == rtk::TIER_BASIC ? RT_QUEUE_GUIDE_BASIC : RT_QUEUE_GUIDE));
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
     F.pixel_sample_scale = fd->pixel_sample_scale;
