@@ -1919,28 +1919,23 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_SHADE_BATCH_FLAT 64
 #endif
 #ifndef RT_QUEUE_CHUNK
-#define RT_QUEUE_CHUNK 256  // most items a wave takes per queue atomic (>= 64)
+// most entries a wave takes per queue atomic, with chunks shrinking as
+// left / (waves x RT_QUEUE_GUIDE): 512 / 16 against 256 / 8 -- half the
+// counter's atomics early, smaller pools late -- C2 186.3 -> 185.0 ms frame
+// and 1/8 shard 24.8 -> 24.4, C4 188.6 -> 186.2 and 29.8 -> 26.7, C3 +-0.5 %
+// (A/B, 2 interleaved reps each; 512 at guide 8: C2 frame -1.1 % but shard
+// +11 %; 512 / 32 and 1024 / 32: C2 shard +4-5 %)
+#define RT_QUEUE_CHUNK 512
 #endif
 #ifndef RT_QUEUE_CHUNK_MESH
-// the mesh tier's cap: its rounds are long (a dependent global load per walk
-// step) and a pool of 256 entries can outlive the queue by milliseconds, but
-// smaller caps cost the whole frame more in counter contention than they
-// save at the end (C4: 128 -> +2 % frame, 1/8 shard 30.0 -> 27.3 ms; 64 ->
-// +6 %, 27.2 ms)
+// the mesh tier's cap, a knob: its rounds are long (a dependent global load
+// per walk step) and a large pool can outlive the queue by milliseconds, but
+// smaller caps cost the whole frame in counter contention (at guide 8, cap
+// 128: C4 frame +2 %, 1/8 shard 30.0 -> 27.3 ms; 64: +6 %, 27.2 ms)
 #define RT_QUEUE_CHUNK_MESH RT_QUEUE_CHUNK
 #endif
-#ifndef RT_QUEUE_CHUNK_BASIC
-// the basic tier (C2): twice the cap with chunks shrinking twice as fast
-// (guide 16): half the counter's atomics early, smaller pools late -- C2
-// 186.3 -> 184.8 ms frame, 1/8 shard 24.8 -> 24.3 ms (A/B, 2 interleaved
-// reps; cap 512 at guide 8: frame -1.1 % but the shard +11 %)
-#define RT_QUEUE_CHUNK_BASIC 512
-#endif
-#ifndef RT_QUEUE_GUIDE_BASIC
-#define RT_QUEUE_GUIDE_BASIC 16
-#endif
 #ifndef RT_QUEUE_GUIDE
-#define RT_QUEUE_GUIDE 8  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
+#define RT_QUEUE_GUIDE 16  // guided chunks: left / (waves * GUIDE), 0 = fixed RT_QUEUE_CHUNK
 #endif
 #ifndef RT_MESH_WAVES
 #define RT_MESH_WAVES 4  // beats 2 waves (164.7 vs 263.8 ms, C4 64 spp) and 3 / 5 waves (+16 % / +12 %)
@@ -2077,9 +2072,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             {
                 const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
                 const uint32_t g = max((uint32_t)((float)left * F.inv_guide), F.chunk_min);
-                constexpr uint32_t CAP = TIER == TIER_MESH    ? RT_QUEUE_CHUNK_MESH
-                                         : TIER == TIER_BASIC ? RT_QUEUE_CHUNK_BASIC
-                                                              : RT_QUEUE_CHUNK;
+                constexpr uint32_t CAP = TIER == TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK;
                 chunk = max(min(g, CAP), avail < n ? n - avail : 0u);
             }
 #endif
@@ -2487,8 +2480,7 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.inv_parts = inv_up(F.parts);
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
-    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) *
-                                 (tier == rtk::TIER_BASIC ? RT_QUEUE_GUIDE_BASIC : RT_QUEUE_GUIDE));
+    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
     F.pixel_sample_scale = fd->pixel_sample_scale;
