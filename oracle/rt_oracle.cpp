@@ -65,6 +65,7 @@ Perlin::Perlin(uint64_t seed) {
     SplitMix64 g(seed);
     for (int i = 0; i < 256; ++i) {
         double r1 = g.next_f64(), r2 = g.next_f64();
+        // host-side construction: glibc in both builds, as the product library's scene builder
         double x = std::cos(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
         double y = std::sin(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
         double z = 1.0 - 2.0 * r2;
@@ -216,8 +217,8 @@ Sphere::Sphere(const Point3& c1, const Point3& c2, double r, std::shared_ptr<Mat
 }
 // sphere.rs:53-61
 void Sphere::get_sphere_uv(const Vec3& p, double& u, double& v) {
-    double theta = std::acos(-p.y());
-    double phi = std::atan2(-p.z(), p.x()) + PI;
+    double theta = m::acos(-p.y());
+    double phi = m::atan2(-p.z(), p.x()) + PI;
     u = phi / (2.0 * PI);
     v = theta / PI;
 }
@@ -263,8 +264,8 @@ Vec3 Sphere::random(const Point3& o) const {
     double r2 = Random::f64();
     double y = 1.0 + r2 * (std::sqrt(1.0 - radius * radius / distance_squared) - 1.0);
     double phi = 2.0 * PI * r1;
-    double x = std::cos(phi) * std::sqrt(1.0 - y * y);
-    double z = std::sin(phi) * std::sqrt(1.0 - y * y);
+    double x = m::cos(phi) * std::sqrt(1.0 - y * y);
+    double z = m::sin(phi) * std::sqrt(1.0 - y * y);
     return expect_unit(uvw.onb_to_world(Vec3(x, y, z)), "sphere random unwrap");
 }
 
@@ -425,7 +426,7 @@ std::optional<HitRecord> ConstantMedium::hit(const Ray& r, const Interval& inter
     double distance_inside_boundary = (t2 - t1) * ray_length;
     PathRng* rng = current_rng();
     if (!rng) throw Panic("medium outside a render path");
-    double hit_distance = neg_inv_density * std::log(rng->medium(medium_id));
+    double hit_distance = neg_inv_density * m::log(rng->medium(medium_id));
     if (hit_distance > distance_inside_boundary) return std::nullopt;
     double t = t1 + hit_distance / ray_length;
     Point3 p = r.at(t);
@@ -478,8 +479,8 @@ Ray Camera::get_ray(uint32_t i, uint32_t j, uint32_t s_i, uint32_t s_j) const {
 // environment.rs:14-24
 Color Camera::background_value(const Ray& r) const {
     Vec3 p = expect_unit(r.dir, "The direction can't be normalized!");
-    double theta = std::acos(-p.y());
-    double phi = PI - std::atan2(-p.z(), p.x());
+    double theta = m::acos(-p.y());
+    double phi = PI - m::atan2(-p.z(), p.x());
     double u = phi / (2.0 * PI);
     double v = theta / PI;
     if (!background) return Color();

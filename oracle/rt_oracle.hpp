@@ -31,8 +31,34 @@
 #include <vector>
 
 #include "rng_contract.hpp"
+#ifdef ORC_CRMATH
+// liboracle_cr.so only: the render path's libm calls go to the kernel's
+// correctly rounded functions instead of glibc, so that a GPU-vs-oracle
+// comparison isolates everything but libm (tests/test_parity_gpu.py: RMSE 0,
+// no diverged sums).  The default liboracle.so calls glibc, as Rust's f64
+// functions do on Linux.
+#include "../raytracer-2025_amd/csrc/rt_crmath.h"
+#endif
 
 namespace orc {
+
+// The path's transcendentals (vec3.rs:63-69, 313-343; sphere.rs:53-61;
+// environment.rs:14-24; volume.rs:58; texture.rs:191-196)
+namespace m {
+#ifdef ORC_CRMATH
+inline double sin(double x) { return rtcr::sin(x); }
+inline double cos(double x) { return rtcr::cos(x); }
+inline double log(double x) { return rtcr::log(x); }
+inline double acos(double x) { return rtcr::acos(x); }
+inline double atan2(double y, double x) { return rtcr::atan2(y, x); }
+#else
+inline double sin(double x) { return std::sin(x); }
+inline double cos(double x) { return std::cos(x); }
+inline double log(double x) { return std::log(x); }
+inline double acos(double x) { return std::acos(x); }
+inline double atan2(double y, double x) { return std::atan2(y, x); }
+#endif
+}  // namespace m
 
 constexpr double PI = 3.14159265358979323846264338327950288;
 constexpr double INF = std::numeric_limits<double>::infinity();
@@ -141,14 +167,14 @@ struct Random {
 inline Vec3 random_in_unit_disk() {
     double theta = Random::random_range(0.0, 2.0 * PI);
     double r = std::sqrt(Random::f64());
-    return Vec3(r * std::cos(theta), r * std::sin(theta), 0.0);
+    return Vec3(r * m::cos(theta), r * m::sin(theta), 0.0);
 }
 // vec3.rs:313-322
 inline Vec3 random_unit_vector() {
     double r1 = Random::f64();
     double r2 = Random::f64();
-    double x = std::cos(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
-    double y = std::sin(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
+    double x = m::cos(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
+    double y = m::sin(2.0 * PI * r1) * 2.0 * std::sqrt(r2 * (1.0 - r2));
     double z = 1.0 - 2.0 * r2;
     return Vec3(x, y, z);
 }
@@ -157,9 +183,9 @@ inline Vec3 random_cosine_direction() {
     double r1 = Random::f64();
     double r2 = Random::f64();
     double phi = 2.0 * PI * r1;
-    double x = std::sin(phi) * std::sqrt(r2);
+    double x = m::sin(phi) * std::sqrt(r2);
     double y = std::sqrt(1.0 - r2);
-    double z = std::cos(phi) * std::sqrt(r2);
+    double z = m::cos(phi) * std::sqrt(r2);
     return Vec3(x, y, z);
 }
 // vec3.rs:345-354
@@ -411,7 +437,7 @@ struct NoiseTexture : Texture {  // texture.rs:177-196
     double scale;
     NoiseTexture(double s, uint64_t seed) : noise(seed), scale(s) {}
     Color value(double, double, const Point3& p) const override {
-        return Color(0.5, 0.5, 0.5) * (1.0 + std::sin(scale * p.z() + 10.0 * noise.turb(p, 7)));
+        return Color(0.5, 0.5, 0.5) * (1.0 + m::sin(scale * p.z() + 10.0 * noise.turb(p, 7)));
     }
 };
 

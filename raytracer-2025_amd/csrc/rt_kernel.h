@@ -111,6 +111,8 @@ extern "C" uint32_t rtk_row_parts(uint32_t W, uint32_t H, uint32_t S, uint32_t p
 extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice, float* out, uint32_t rows, uint32_t W,
                                               uint32_t parts, hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream);
+extern "C" hipError_t rtk_launch_math(int fn, int impl, const double* a, const double* b, double* out, uint64_t n,
+                                      hipStream_t stream);
 // device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);

@@ -19,6 +19,7 @@
 // in LDS, laid out [depth][lane] so a wave's pushes/pops hit 64 distinct banks.
 #include <hip/hip_runtime.h>
 
+#include "rt_crmath.h"
 #include "rt_kernel.h"
 #include "rt_math.h"
 #include "rt_slab.h"
@@ -221,7 +222,7 @@ __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
                     weight = 0.5 * weight;
                 }
                 const double turb = fabs(accum);
-                return (1.0 + sin(t.scale * p.z + 10.0 * turb)) * d3(0.5, 0.5, 0.5);
+                return (1.0 + k_sin(t.scale * p.z + 10.0 * turb)) * d3(0.5, 0.5, 0.5);
             }
             default: break;
           }
@@ -780,7 +781,7 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
     if (t1 < 0.0) t1 = 0.0;
     const double ray_length = len(r.d);
     const double inside = (t2 - t1) * ray_length;
-    const double hd = M.neg_inv_density * log(rng.medium(M.medium_id));
+    const double hd = M.neg_inv_density * k_log(rng.medium(M.medium_id));
     if (hd > inside) return false;
     t = t1 + hd / ray_length;  // volume.rs:65
     return t <= tmax;
@@ -1388,8 +1389,8 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
         outward = divs(p - c, radius);  // sphere.rs:99
         if (S.materials[rec.mat].flags & MF_NEEDS_UV) {
             // sphere.rs:53-61
-            const double theta = acos(-outward.y);
-            const double phi = atan2(-outward.z, outward.x) + PI;
+            const double theta = k_acos(-outward.y);
+            const double phi = k_atan2(-outward.z, outward.x) + PI;
             rec.u = phi / (2.0 * PI);
             rec.v = theta / PI;
         }
@@ -1523,7 +1524,9 @@ __device__ __forceinline__ D3 light_random_one(const SceneView& S, uint32_t ref,
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
     const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
     const double phi = 2.0 * PI * r1;
-    const double x = cos(phi) * sqrt(1.0 - y * y), z = sin(phi) * sqrt(1.0 - y * y);
+    double sphi, cphi;
+    k_sincos(phi, &sphi, &cphi);
+    const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
     const D3 wv = onb_world(nd, d3(x, y, z), ok2);
     bool ok3;
     const D3 res = unit(wv, ok3);
@@ -1619,7 +1622,9 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
         const double r1 = rng.next(ovf), r2 = rng.next(ovf);
         const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
         const double phi = 2.0 * PI * r1;
-        const double x = cos(phi) * sqrt(1.0 - y * y), z = sin(phi) * sqrt(1.0 - y * y);
+        double sphi, cphi;
+        k_sincos(phi, &sphi, &cphi);
+        const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
         const D3 res = unit(onb_world(nd, d3(x, y, z), ok2), ok3);
         ok = ok1 && ok2 && ok3;
         return res;
@@ -1642,7 +1647,7 @@ __device__ __forceinline__ D3 mat_tex(const SceneView& S, const DMaterial& M, do
 __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
     double sn, cs;
-    sincos(2.0 * PI * r1, &sn, &cs);
+    k_sincos(2.0 * PI * r1, &sn, &cs);
     const double s = sqrt(r2 * (1.0 - r2));
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
@@ -1697,8 +1702,8 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             if (!ok) panic = true;
             double u = 0.0, v = 0.0;
             if (FULL && S.textures[S.background_tex].needs_uv) {
-                const double theta = acos(-p.y);
-                const double phi = PI - atan2(-p.z, p.x);
+                const double theta = k_acos(-p.y);
+                const double phi = PI - k_atan2(-p.z, p.x);
                 u = phi / (2.0 * PI);
                 v = theta / PI;
             }
@@ -1718,7 +1723,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     if constexpr (HOIST) {
         xi0 = rng.next(ovf);
         xi1 = rng.next(ovf);
-        sincos(2.0 * PI * xi0, &sn0, &cs0);
+        k_sincos(2.0 * PI * xi0, &sn0, &cs0);
     }
     if constexpr (TIER == TIER_FULL_GL) {
         if (M.flags & MF_EMISSIVE) L = L + beta * emitted_tree<RT_MAT_DEPTH>(S, rec.mat, rec.u, rec.v, rec.p);
@@ -1841,7 +1846,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 if constexpr (!HOIST) {
                     const double r1 = rng.next(ovf);
                     r2 = rng.next(ovf);
-                    sincos(2.0 * PI * r1, &sn, &cs);
+                    k_sincos(2.0 * PI * r1, &sn, &cs);
                 }
                 const double sr2 = sqrt(r2);
                 dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
@@ -2131,7 +2136,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
                 const double rr = sqrt(rng.next(ovf));
                 double sn, cs;
-                sincos(theta, &sn, &cs);
+                k_sincos(theta, &sn, &cs);
                 origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
             }
             ray.o = origin;
@@ -2411,6 +2416,41 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     }
 }
 
+// Math self-test (rt_math_selftest): the kernel's f64 functions (impl 0,
+// rt_crmath.h) or ROCm's device libm (impl 1, ocml) on n arguments.
+__global__ void __launch_bounds__(256) rt_math_kernel(int fn, int impl, const double* __restrict__ a,
+                                                     const double* __restrict__ b, double* __restrict__ out,
+                                                     uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i], y = b ? b[i] : 0.0;
+    double r = 0.0, s = 0.0, c = 0.0;
+    if (impl == 0) {
+        switch (fn) {
+            case 0: r = rtcr::sin(x); break;
+            case 1: r = rtcr::cos(x); break;
+            case 2: rtcr::sincos(x, &s, &c), r = s; break;
+            case 3: rtcr::sincos(x, &s, &c), r = c; break;
+            case 4: r = rtcr::log(x); break;
+            case 5: r = rtcr::acos(x); break;
+            case 6: r = rtcr::atan2(x, y); break;
+            default: r = sqrt(x); break;
+        }
+    } else {
+        switch (fn) {
+            case 0: r = ::sin(x); break;
+            case 1: r = ::cos(x); break;
+            case 2: ::sincos(x, &s, &c), r = s; break;
+            case 3: ::sincos(x, &s, &c), r = c; break;
+            case 4: r = ::log(x); break;
+            case 5: r = ::acos(x); break;
+            case 6: r = ::atan2(x, y); break;
+            default: r = ::sqrt(x); break;
+        }
+    }
+    out[i] = r;
+}
+
 // to_rgb of a linear f32 framebuffer already on the device (e.g. the gathered
 // multi-GPU frame).
 __global__ void __launch_bounds__(256) rt_to_rgb_kernel(const float* __restrict__ lin, uint8_t* __restrict__ srgb,
@@ -2519,6 +2559,14 @@ extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rtk::rt_deinterleave_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, staging,
                        (uint64_t)slice, out, rows, W, parts);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_math(int fn, int impl, const double* a, const double* b, double* out, uint64_t n,
+                                      hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rtk::rt_math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, fn, impl, a, b, out,
+                       n);
     return hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rt_crmath.h"
+
 namespace rtk {
 
 constexpr double PI = 3.14159265358979323846264338327950288;
@@ -41,6 +43,26 @@ __device__ __forceinline__ D3 reflect(D3 v, D3 n) { return v - (2.0 * dot(v, n))
 __device__ __forceinline__ D3 mat3(const double* m, D3 v) {
     return d3(m[0] * v.x + m[1] * v.y + m[2] * v.z, m[3] * v.x + m[4] * v.y + m[5] * v.z,
               m[6] * v.x + m[7] * v.y + m[8] * v.z);
+}
+
+// ---------------------------------------------------------------- libm
+// The transcendentals of the path: correctly rounded (rt_crmath.h), so that
+// they agree with glibc -- what Rust's f64::sin / cos / ln / acos / atan2 call
+// -- wherever glibc is correctly rounded (~99.9 % of arguments); RT_CRMATH=0
+// selects ROCm's ocml (A/B only: it differs from glibc by an ulp far more
+// often, tests/test_crmath_gpu.py).
+#ifndef RT_CRMATH
+#define RT_CRMATH 1
+#endif
+__device__ __forceinline__ double k_sin(double x) { return RT_CRMATH ? rtcr::sin(x) : ::sin(x); }
+__device__ __forceinline__ double k_log(double x) { return RT_CRMATH ? rtcr::log(x) : ::log(x); }
+__device__ __forceinline__ double k_acos(double x) { return RT_CRMATH ? rtcr::acos(x) : ::acos(x); }
+__device__ __forceinline__ double k_atan2(double y, double x) { return RT_CRMATH ? rtcr::atan2(y, x) : ::atan2(y, x); }
+__device__ __forceinline__ void k_sincos(double x, double* s, double* c) {
+    if (RT_CRMATH)
+        rtcr::sincos(x, s, c);
+    else
+        ::sincos(x, s, c);
 }
 
 // ---------------------------------------------------------------- RNG

@@ -906,6 +906,30 @@ int32_t rt_to_rgb_device(const float* lin_dev, uint8_t* srgb_dev, uint64_t n_val
     return e == hipSuccess ? RT_OK : hip_fail(e, "to_rgb launch");
 }
 
+int32_t rt_math_selftest(int32_t fn, int32_t impl, const double* a, const double* b, double* out, uint64_t n) {
+    if (fn < 0 || fn > 7 || impl < 0 || impl > 1) return set_error(RT_EINVAL, "unknown function or implementation");
+    if (n && (!a || !out || (fn == 6 && !b))) return set_error(RT_EINVAL, "null argument");
+    if (n == 0) return RT_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, dev)) != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(RT_EDEVICE, std::string("librt_mi355x.so needs a gfx950 device, found ") + prop.gcnArchName);
+    double* d = nullptr;
+    const size_t bytes = n * sizeof(double);
+    if ((e = hipMalloc(&d, bytes * 3)) != hipSuccess) return hip_fail(e, "hipMalloc");
+    int32_t rc = RT_OK;
+    if ((e = hipMemcpy(d, a, bytes, hipMemcpyHostToDevice)) != hipSuccess ||
+        (b && (e = hipMemcpy(d + n, b, bytes, hipMemcpyHostToDevice)) != hipSuccess) ||
+        (e = rtk_launch_math(fn, impl, d, b ? d + n : nullptr, d + 2 * n, n, nullptr)) != hipSuccess ||
+        (e = hipMemcpy(out, d + 2 * n, bytes, hipMemcpyDeviceToHost)) != hipSuccess)
+        rc = hip_fail(e, "math self-test");
+    (void)hipFree(d);
+    return rc;
+}
+
 int32_t rt_render(rt_scene* s, int32_t world, int32_t lights, const rt_camera* cam, const rt_render_opts* opts,
                   float* out_lin, uint8_t* out_srgb, rt_stats* st) {
     if (!cam) return set_error(RT_EINVAL, "null camera");

@@ -48,6 +48,15 @@ def oracle(capi):
 
 
 @pytest.fixture(scope="session")
+def oracle_cr(capi):
+    """The oracle with its path libm calls on rt_crmath.h (liboracle_cr.so):
+    isolates everything but glibc's own misroundings."""
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_cr.so")
+    _make(os.path.join(ROOT, "oracle"))
+    return capi.Api(ctypes.CDLL(so), "orc_", capi.ORACLE_EXTRAS)
+
+
+@pytest.fixture(scope="session")
 def product():
     """librt_mi355x.so through the package loader (fails loudly when missing)."""
     pkg = pkg_module()

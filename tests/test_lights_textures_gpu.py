@@ -145,6 +145,31 @@ def test_lights_without_pdf_panic(gpu, oracle, rt, capi, kind):
         assert e.value.code == -5  # RT_EPANIC
 
 
+def checker_world(rt, s, where):
+    """CheckerTexture (texture.rs:39-73) on spheres and a floor; "quad_y0" puts
+    the floor on y = 0, the texture's knife edge."""
+    even = s.CheckerTexture(0.5, s.SolidColor((0.9, 0.9, 0.9)), s.SolidColor((0.1, 0.3, 0.6)))
+    tex = s.CheckerTexture(3.0, even, s.SolidColor((0.8, 0.2, 0.1)))
+    world = s.Hittables()
+    if where == "sphere":
+        world.add(s.Sphere((0, -1000, 0), 1000, s.Lambertian(tex)))
+    else:
+        y = 0.0 if where == "quad_y0" else 0.25
+        world.add(s.Quad((-8, y, -8), (16, 0, 0), (0, 0, 16), s.Lambertian(tex)))
+    world.add(s.Sphere((0, 1, 0), 1.0, s.Lambertian(tex)))
+    world.add(s.Sphere((2.2, 0.7, 0.5), 0.7, s.Metal((0.8, 0.8, 0.8), 0.05)))
+    cam = rt.Camera()
+    cam.aspect_ratio = 16 / 9
+    cam.image_width = 96
+    cam.samples_per_pixel = 16
+    cam.max_depth = 20
+    cam.vertical_fov_in_degrees = 30.0
+    cam.look_from = (6.0, 2.5, 7.0)
+    cam.look_at = (0.0, 0.6, 0.0)
+    cam.background = s.SkyGradient()
+    return world, None, cam
+
+
 @pytest.mark.parametrize("where", ["sphere", "quad", "quad_y0"])
 def test_checker_texture(gpu, oracle, rt, capi, where):
     """CheckerTexture (texture.rs:39-73): floor(scale * p) parity, nested
@@ -153,44 +178,17 @@ def test_checker_texture(gpu, oracle, rt, capi, where):
 
     quad_y0 puts the floor on y = 0, a knife edge of the texture: every hit
     point's p.y is 0 +- an ulp, and floor(p.y / 0.5) is 0 or -1 by its sign,
-    so an ulp of difference anywhere upstream (f64 sin / cos of ROCm's ocml
-    against glibc in a bounce direction) picks the other square.  Measured:
-    1.3e-3 of its (pixel, s_i) sums diverged, RMSE (5.6e-4, 5.6e-4, 1.1e-3)
-    -- the blue channel a hair above the north-star bar, which no f64 path
-    with a different libm can hold on a knife edge; with contraction on (a
-    fused hit point) half of the sums diverged, which is why the kernel is
-    built with -ffp-contract=off."""
-    def build(s):
-        even = s.CheckerTexture(0.5, s.SolidColor((0.9, 0.9, 0.9)), s.SolidColor((0.1, 0.3, 0.6)))
-        tex = s.CheckerTexture(3.0, even, s.SolidColor((0.8, 0.2, 0.1)))
-        world = s.Hittables()
-        if where == "sphere":
-            world.add(s.Sphere((0, -1000, 0), 1000, s.Lambertian(tex)))
-        else:
-            y = 0.0 if where == "quad_y0" else 0.25
-            world.add(s.Quad((-8, y, -8), (16, 0, 0), (0, 0, 16), s.Lambertian(tex)))
-        world.add(s.Sphere((0, 1, 0), 1.0, s.Lambertian(tex)))
-        world.add(s.Sphere((2.2, 0.7, 0.5), 0.7, s.Metal((0.8, 0.8, 0.8), 0.05)))
-        cam = rt.Camera()
-        cam.aspect_ratio = 16 / 9
-        cam.image_width = 96
-        cam.samples_per_pixel = 16
-        cam.max_depth = 20
-        cam.vertical_fov_in_degrees = 30.0
-        cam.look_from = (6.0, 2.5, 7.0)
-        cam.look_at = (0.0, 0.6, 0.0)
-        cam.background = s.SkyGradient()
-        return world, None, cam
-    out, st = render_both(gpu, oracle, rt, build)
-    if where == "quad_y0":
-        g, o = out["gpu"][0], out["oracle"][0]
-        assert np.all(rmse_per_channel(g, o) < 2e-3)
-        check(out, tol=2e-3, min_exact=0.98, max_div=5e-3)
-    else:
-        check(out)
+    so an ulp of difference anywhere upstream picks the other square.  With
+    ROCm's ocml sin / cos in the kernel 1.3e-3 of its (pixel, s_i) sums
+    diverged (RMSE 1.1e-3, round 2); with the kernel's correctly rounded
+    functions (rt_crmath.h) only glibc's own misroundings remain, and the
+    default bar holds (test_libm_parity_gpu.py: exact against the oracle on
+    the same functions)."""
+    out, st = render_both(gpu, oracle, rt, lambda s: checker_world(rt, s, where))
+    check(out)
     assert st["gpu"].panics == 0
     s = rt.Scene(gpu)
-    w, l, c = build(s)
+    w, l, c = checker_world(rt, s, where)
     assert _tier(gpu, capi, s, w, l, c) == (0 if where == "sphere" else 1)
 
 

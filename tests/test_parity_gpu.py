@@ -437,11 +437,12 @@ def test_c4_obj_full_tier_materials(gpu, oracle, rt, tmp_path):
 
 
 def test_c4_full_size_mesh_rows(gpu, oracle, rt, scenes, tmp_path):
-    """BASELINE configs[3] geometry: the 1M-triangle terrain at 1920x1080.  Two
-    shard rows (0 and 540) at 4 spp against the oracle on the same 1M-triangle
-    world, and the whole frame at 1 spp for finiteness / no panics."""
+    """BASELINE configs[3]: the 1M-triangle terrain at 1920x1080, 256 spp
+    (16^2), depth 50.  Two shard rows (0 and 540) at the config's full sample
+    count against the oracle on the same 1M-triangle world, and the whole
+    frame at 1 spp for finiteness / no panics."""
     p = scenes.write_terrain_obj(str(tmp_path), 707)
-    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, lambda s: scenes.obj_terrain(s, p, 1920, 4), 11, [(0, 540)],
+    g, o, gp, op = rows_vs_oracle(gpu, oracle, rt, lambda s: scenes.obj_terrain(s, p, 1920, 256), 11, [(0, 540)],
                                   full_spp=1)
     assert g.shape == (2, 1920, 3)
     check({"gpu": (g, None, gp), "oracle": (o, None, op)})
