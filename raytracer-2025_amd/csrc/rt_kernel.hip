@@ -22,6 +22,7 @@
 #include "rt_crmath.h"
 #include "rt_kernel.h"
 #include "rt_math.h"
+#include "rt_qnode.h"
 #include "rt_slab.h"
 #include "rt_sphere_filter.h"
 
@@ -980,16 +981,26 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
         const bool planar = kind == K_TRI || kind == K_QUAD;
         // (the array addresses as values, selected: a select between the
         // SceneView's members made the compiler index a scratch copy of it)
-        const uint64_t a_node = (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars, a_sphere = (uint64_t)S.spheres;
+        const bool qn = S.qnodes != 0;
+        const uint64_t a_node = qn ? (uint64_t)S.nodes4q : (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars,
+                       a_sphere = (uint64_t)S.spheres;
         uint64_t addr = a_node;
         uint32_t stride = 0u;
-        if (kind == K_BVH) stride = (uint32_t)sizeof(DNode4);
+        if (kind == K_BVH) stride = qn ? (uint32_t)sizeof(DNode4Q) : (uint32_t)sizeof(DNode4);
         if (planar) addr = a_planar, stride = (uint32_t)sizeof(DPlanar);
         if (kind == K_SPHERE) addr = a_sphere, stride = (uint32_t)sizeof(double4);
         const RT_GLOBAL float4* q = reinterpret_cast<const RT_GLOBAL float4*>(addr + (uint64_t)idx * stride);
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6], q7 = q[7];
+        // rows 0-3 hold a quantized node, a sphere (2) and half a planar
+        // record; the rest only for the lanes whose record has them
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4, q7 = q4;
+        if (planar || (kind == K_BVH && !qn)) q4 = q[4], q5 = q[5], q6 = q[6];
+        if (planar) q7 = q[7];
         if (kind == K_BVH) {
-            T.cur = visit4_boxes_rows(q0, q1, q2, q3, q4, q5, q6, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
+            if (qn)
+                T.cur = visit4q_rows(q0, q1, q2, q3, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
+            else
+                T.cur = visit4_boxes_rows(q0, q1, q2, q3, q4, q5, q6, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
         } else if (kind == K_SPHERE) {
             got = sphere_t_inv(d3(f4_lo(q0), f4_hi(q0), f4_lo(q1)), f4_hi(q1), r, T.a, T.inva, tmin, T.cl.c, t);
         } else if (planar) {
@@ -1216,16 +1227,10 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
 // and the others pushed farthest first -- primitives included, so a triangle
 // is tested (planar_t) when the walk reaches it, in distance order.
 template <class Stack>
-__device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const float4 ly, const float4 lz,
-                                                      const float4 hx, const float4 hy, const float4 hz,
-                                                      const float4 rq, const RayF& rf, float tmin_f, float c_f,
-                                                      Stack& stk, uint32_t& sp);
-template <class Stack>
-__device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
-                                                 float c_f, Stack& stk, uint32_t& sp) {
-    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
-    return visit4_boxes_rows(np[0], np[1], np[2], np[3], np[4], np[5], np[6], rf, tmin_f, c_f, stk, sp);
-}
+__device__ __forceinline__ uint32_t visit4_core(const float LX[4], const float LY[4], const float LZ[4],
+                                                const float HX[4], const float HY[4], const float HZ[4],
+                                                const uint32_t R[4], const RayF& rf, float tmin_f, float c_f,
+                                                Stack& stk, uint32_t& sp);
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const float4 ly, const float4 lz,
                                                       const float4 hx, const float4 hy, const float4 hz,
@@ -1234,6 +1239,47 @@ __device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const flo
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
+    return visit4_core(LX, LY, LZ, HX, HY, HZ, R, rf, tmin_f, c_f, stk, sp);
+}
+// A DNode4Q's four rows (rt_layout.h): the children's boxes decoded as
+// fmaf(q, scale, origin) (rt_qnode.h) -- boxes that contain the f32 boxes
+// the 112-B node stores -- then the same visit.
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4q_rows(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
+                                                 const RayF& rf, float tmin_f, float c_f, Stack& stk, uint32_t& sp) {
+    const uint32_t ex = __float_as_uint(r0.w);
+    const float sx = __uint_as_float((ex & 0xffu) << 23), sy = __uint_as_float(((ex >> 8) & 0xffu) << 23),
+                sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
+    const uint32_t qlx = __float_as_uint(r1.x), qly = __float_as_uint(r1.y), qlz = __float_as_uint(r1.z);
+    const uint32_t qhx = __float_as_uint(r1.w), qhy = __float_as_uint(r2.x), qhz = __float_as_uint(r2.y);
+    float LX[4], LY[4], LZ[4], HX[4], HY[4], HZ[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        LX[i] = qnode_decode(r0.x, sx, (qlx >> (8 * i)) & 0xffu);
+        LY[i] = qnode_decode(r0.y, sy, (qly >> (8 * i)) & 0xffu);
+        LZ[i] = qnode_decode(r0.z, sz, (qlz >> (8 * i)) & 0xffu);
+        HX[i] = qnode_decode(r0.x, sx, (qhx >> (8 * i)) & 0xffu);
+        HY[i] = qnode_decode(r0.y, sy, (qhy >> (8 * i)) & 0xffu);
+        HZ[i] = qnode_decode(r0.z, sz, (qhz >> (8 * i)) & 0xffu);
+    }
+    const uint32_t R[4] = {__float_as_uint(r3.x), __float_as_uint(r3.y), __float_as_uint(r3.z), __float_as_uint(r3.w)};
+    return visit4_core(LX, LY, LZ, HX, HY, HZ, R, rf, tmin_f, c_f, stk, sp);
+}
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
+                                                 float c_f, Stack& stk, uint32_t& sp) {
+    if (S.qnodes) {
+        const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4q + idx);
+        return visit4q_rows(np[0], np[1], np[2], np[3], rf, tmin_f, c_f, stk, sp);
+    }
+    const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
+    return visit4_boxes_rows(np[0], np[1], np[2], np[3], np[4], np[5], np[6], rf, tmin_f, c_f, stk, sp);
+}
+template <class Stack>
+__device__ __forceinline__ uint32_t visit4_core(const float LX[4], const float LY[4], const float LZ[4],
+                                                const float HX[4], const float HY[4], const float HZ[4],
+                                                const uint32_t R[4], const RayF& rf, float tmin_f, float c_f,
+                                                Stack& stk, uint32_t& sp) {
     constexpr float INF = __builtin_huge_valf();
     float key[4];
     uint32_t ref[4];

@@ -229,6 +229,12 @@ static int prepare_tier(HostWorld& hw) {
             return -1;
         }
     }
+    // mesh / full tiers: 64-B quantized nodes (rt_qnode.h) unless a bound is
+    // not finite (then the 112-B f32 nodes); RT_QNODES=0 keeps f32 nodes (A/B)
+    if (tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
+        const char* q = std::getenv("RT_QNODES");
+        if (!(q && q[0] == '0')) bvh4_quantize(hw);
+    }
     return tier;
 }
 
@@ -287,6 +293,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     rtk::SceneView& v = fw.rel;
     v.nodes = (const rtk::DNode*)off(put(blob, hw.nodes));
     v.nodes4 = (const rtk::DNode4*)off(put(blob, hw.nodes4));
+    v.nodes4q = (const rtk::DNode4Q*)off(put(blob, hw.nodes4q));
     v.spheres = (const double4*)off(put(blob, hw.spheres));
     v.sphere_mat = (const int32_t*)off(put(blob, hw.sphere_mat));
     v.msph_center = (const double4*)off(put(blob, hw.msph_center));
@@ -317,6 +324,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.stack_need = hw.stack_need;
     v.features = hw.features;
     v.n_nodes4 = (uint32_t)hw.nodes4.size();
+    v.qnodes = hw.qnodes ? 1u : 0u;
     v.n_perlin = (uint32_t)hw.perlin.size();
     fw.tier = tier;
     fw.stack_need = hw.stack_need;
@@ -400,7 +408,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     char* b = d->blob;
     rtk::SceneView v = fw.rel;
     auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
-    fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
+    fix(v.nodes), fix(v.nodes4), fix(v.nodes4q), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
         fix(v.msph_mat), fix(v.planars), fix(v.planars_f), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
         fix(v.remap_nm), fix(v.list_children), fix(v.list_boxes), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
         fix(v.texels), fix(v.perlin);
@@ -852,6 +860,7 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
         const int tier = prepare_tier(hw);
         if (tier < 0) return RT_ESTACK;
         if (!hw.nodes4.empty()) out->bvh_nodes = (uint32_t)hw.nodes4.size();
+        if (hw.qnodes) out->bvh_nodes = (uint32_t)hw.nodes4q.size();
         out->stack_need = hw.stack_need;
         out->kernel_tier = (uint32_t)tier;
         out->features = hw.features;

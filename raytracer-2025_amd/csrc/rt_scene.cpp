@@ -2,6 +2,7 @@
 // world flattener.  Host code only; the device half is rt_render.hip.
 #include "rt_kernel.h"
 #include "rt_png.hpp"
+#include "rt_qnode.h"
 #include "rt_scene.hpp"
 
 #include <algorithm>
@@ -1435,5 +1436,22 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
     hw.world_root = root;
     hw.stack_need = sn;
     return sn;
+}
+
+bool bvh4_quantize(HostWorld& hw) {
+    std::vector<rtk::DNode4Q> q(hw.nodes4.size());
+    for (size_t k = 0; k < hw.nodes4.size(); ++k) {
+        QNode e;
+        if (!qnode_encode(hw.nodes4[k].lo, hw.nodes4[k].hi, hw.nodes4[k].ref, e)) return false;
+        rtk::DNode4Q& n = q[k];
+        n = rtk::DNode4Q{};
+        for (int a = 0; a < 3; ++a) n.origin[a] = e.origin[a], n.qlo[a] = e.qlo[a], n.qhi[a] = e.qhi[a];
+        n.exps = e.exps;
+        for (int i = 0; i < 4; ++i) n.ref[i] = hw.nodes4[k].ref[i];
+    }
+    hw.nodes4q = std::move(q);
+    hw.nodes4.clear();
+    hw.qnodes = true;
+    return true;
 }
 }  // namespace rth

@@ -107,7 +107,9 @@ struct MatRec {
 // Flattened world on the host, ready to upload as one blob.
 struct HostWorld {
     std::vector<rtk::DNode> nodes;
-    std::vector<rtk::DNode4> nodes4;  // basic tier (bvh4_basic)
+    std::vector<rtk::DNode4> nodes4;  // basic tier (bvh4_basic); mesh / full tiers before bvh4_quantize
+    std::vector<rtk::DNode4Q> nodes4q;  // mesh / full tiers: quantized nodes (qnodes)
+    bool qnodes = false;
     std::vector<double4> spheres;
     std::vector<int32_t> sphere_mat;
     std::vector<double4> msph_center, msph_dir;
@@ -163,5 +165,9 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 // unchanged when it exceeds max_need), or UINT32_MAX (hw unchanged) when the
 // tree would have more than max_nodes nodes.
 uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes = SIZE_MAX);
+// Mesh / full tiers: re-encodes hw.nodes4 (boxed children only) as 64-B
+// quantized nodes (hw.nodes4q, rt_qnode.h) and sets hw.qnodes; false (hw
+// unchanged) when a node's bounds are not finite or span more than 2^100.
+bool bvh4_quantize(HostWorld& hw);
 void destroy_render_state(RenderState* r);
 }  // namespace rth

@@ -2,7 +2,9 @@
 """Interleaved A/B of kernel variants (raytracer-2025_amd/librt_ab_*.so, built
 by `make -C raytracer-2025_amd ab`) in one process on the C2 scene: each
 variant renders the same frame; path-kernel time from the library's HIP
-events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]
+events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]; a variant is a library
+name (librt_ab_<name>.so) optionally followed by @VAR=val,... (environment
+variables set while its world is flattened, e.g. base@RT_QNODES=0).
 AB_WORKLOAD=c3|c4|c5 renders that config's scene (C5 at 1920 wide) instead of C2."""
 import ctypes
 import glob
@@ -25,8 +27,17 @@ names = sys.argv[3:] or sorted(os.path.basename(p)[len("librt_ab_"):-3]
                                 for p in glob.glob(os.path.join(ROOT, "raytracer-2025_amd", "librt_ab_*.so")))
 torch.cuda.init()
 runs = {}
+libs = {}
 for n in names:
-    api = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", f"librt_ab_{n}.so")), "rt_")
+    # "lib@VAR=val,VAR2=val": librt_ab_<lib>.so with those environment
+    # variables set while its world is flattened (the first render)
+    lib, _, envs = n.partition("@")
+    env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    if lib not in libs:
+        libs[lib] = capi.Api(ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", f"librt_ab_{lib}.so")), "rt_")
+    api = libs[lib]
     scene = rt.Scene(api)
     wl = os.environ.get("AB_WORKLOAD", "c2")
     if wl == "c3":
@@ -43,6 +54,11 @@ for n in names:
         world, lights, cam = scenes.random_spheres(scene, 1920, spp)
     print("warm-up", n, file=sys.stderr, flush=True)
     lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)  # warm-up
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     runs[n] = (scene, world, lights, cam, lin)
 res = {n: [] for n in names}
 for _ in range(reps):
