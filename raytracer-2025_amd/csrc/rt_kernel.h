@@ -110,6 +110,8 @@ extern "C" uint32_t rtk_row_parts(uint32_t W, uint32_t H, uint32_t S, uint32_t p
 // the frame's `rows` compact rows (rows x W x 3 f32).
 extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice, float* out, uint32_t rows, uint32_t W,
                                               uint32_t parts, hipStream_t stream);
+extern "C" hipError_t rtk_launch_deinterleave_u8(const uint8_t* staging, size_t slice, uint8_t* out, uint32_t rows,
+                                                 uint32_t W, uint32_t parts, hipStream_t stream);
 extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream);
 extern "C" hipError_t rtk_launch_math(int fn, int impl, const double* a, const double* b, double* out, uint64_t n,
                                       hipStream_t stream);

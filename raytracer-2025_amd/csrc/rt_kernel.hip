@@ -2516,6 +2516,17 @@ __global__ void __launch_bounds__(256) rt_deinterleave_kernel(const float* __res
     const uint64_t x = i - (uint64_t)j * row_floats;
     out[i] = staging[(uint64_t)(j % parts) * slice + (uint64_t)(j / parts) * row_floats + x];
 }
+// The same for a gathered shard's to_rgb bytes.
+__global__ void __launch_bounds__(256) rt_deinterleave_u8_kernel(const uint8_t* __restrict__ staging, uint64_t slice,
+                                                                 uint8_t* __restrict__ out, uint32_t rows, uint32_t W,
+                                                                 uint32_t parts) {
+    const uint64_t row_bytes = (uint64_t)W * 3;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)rows * row_bytes) return;
+    const uint32_t j = (uint32_t)(i / row_bytes);
+    const uint64_t x = i - (uint64_t)j * row_bytes;
+    out[i] = staging[(uint64_t)(j % parts) * slice + (uint64_t)(j / parts) * row_bytes + x];
+}
 }  // namespace rtk
 
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
@@ -2604,6 +2615,15 @@ extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice
     const uint64_t n = (uint64_t)rows * W * 3;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(rtk::rt_deinterleave_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, staging,
+                       (uint64_t)slice, out, rows, W, parts);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t rtk_launch_deinterleave_u8(const uint8_t* staging, size_t slice, uint8_t* out, uint32_t rows,
+                                                 uint32_t W, uint32_t parts, hipStream_t stream) {
+    const uint64_t n = (uint64_t)rows * W * 3;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(rtk::rt_deinterleave_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, staging,
                        (uint64_t)slice, out, rows, W, parts);
     return hipGetLastError();
 }

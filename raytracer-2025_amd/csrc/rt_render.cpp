@@ -133,6 +133,8 @@ struct RenderState {
     int root_device = -1;
     float* staging = nullptr;
     size_t staging_bytes = 0;
+    uint8_t* staging_srgb = nullptr;  // the parts' to_rgb bytes, gathered like their f32 rows
+    size_t staging_srgb_bytes = 0;
     float* full = nullptr;  // gathered frame of a host-buffer render
     size_t full_bytes = 0;
     uint8_t* full_srgb = nullptr;
@@ -174,13 +176,14 @@ static void destroy_device_world(DeviceWorld* d) {
 static void free_root_buffers(RenderState* r) {
     if (r->root_device >= 0) (void)hipSetDevice(r->root_device);
     if (r->staging) (void)hipFree(r->staging);
+    if (r->staging_srgb) (void)hipFree(r->staging_srgb);
     if (r->full) (void)hipFree(r->full);
     if (r->full_srgb) (void)hipFree(r->full_srgb);
     if (r->g_start) (void)hipEventDestroy(r->g_start);
     if (r->g_stop) (void)hipEventDestroy(r->g_stop);
     r->staging = r->full = nullptr;
-    r->full_srgb = nullptr;
-    r->staging_bytes = r->full_bytes = r->full_srgb_bytes = 0;
+    r->full_srgb = r->staging_srgb = nullptr;
+    r->staging_bytes = r->full_bytes = r->full_srgb_bytes = r->staging_srgb_bytes = 0;
     r->g_start = r->g_stop = nullptr;
     r->g_recorded = false;
     r->root_device = -1;
@@ -604,6 +607,10 @@ static int32_t root_buffers(RenderState* r, int device, size_t staging_bytes, si
     if ((rc = grow((void**)&r->full, r->full_bytes, full_bytes, "hipMalloc gathered frame")) != RT_OK) return rc;
     if ((rc = grow((void**)&r->full_srgb, r->full_srgb_bytes, srgb_bytes, "hipMalloc gathered srgb")) != RT_OK)
         return rc;
+    const size_t srgb_staging = srgb_bytes ? staging_bytes / sizeof(float) : 0;
+    if ((rc = grow((void**)&r->staging_srgb, r->staging_srgb_bytes, srgb_staging, "hipMalloc gather srgb staging")) !=
+        RT_OK)
+        return rc;
     return RT_OK;
 }
 
@@ -645,6 +652,9 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     if (comm && (comm->rank < 0 || comm->rank >= comm->nranks)) return set_error(RT_EINVAL, "bad communicator");
     const bool reference_bvh = opts && (opts->flags & RT_FLAG_REFERENCE_BVH);
     hipStream_t user_stream = opts ? (hipStream_t)opts->stream : nullptr;
+    // every rank of a host-buffer render sends its to_rgb bytes (the root's
+    // out_srgb decides nothing the other ranks could see)
+    if (comm && host_call) want_srgb = true;
 
     int cur = -1;
     hipError_t e = hipGetDevice(&cur);
@@ -670,7 +680,11 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         p.user_stream = i == 0;
         p.stream = (i == 0) ? user_stream : nullptr;
         p.out = gather ? nullptr : dev_out;  // gathered parts render into the slot's buffer
-        p.want_srgb = want_srgb && !gather;  // a gathered frame's bytes come from its f32 values (to_rgb below)
+        // every part makes its rows' to_rgb bytes from the f64 pixel sums, as
+        // the reference converts its f64 colour (color.rs:27-36); a gathered
+        // frame's bytes are those parts' bytes, not a conversion of its f32
+        // values, so they do not depend on the device count
+        p.want_srgb = want_srgb;
     }
     if (r->slots.size() < parts.size()) r->slots.resize(parts.size(), nullptr);
     FlatWorld fw;
@@ -707,7 +721,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         hipStream_t rs = root.stream;
         if (is_root) {
             const size_t full = (dev_out ? 0 : rows * row_floats * sizeof(float));
-            const size_t srgb = (host_call && want_srgb) ? rows * row_floats : 0;
+            const size_t srgb = want_srgb ? rows * row_floats : 0;
             if ((rc = root_buffers(r, root.device, n_parts * slice * sizeof(float), full, srgb)) != RT_OK) return rc;
             if ((e = hipEventRecord(r->g_start, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
         }
@@ -719,10 +733,15 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
             ncclResult_t ne = nc.group_start();
             if (ne == ncclSuccess)
                 ne = nc.send(root.out_used, (size_t)root.rows * row_floats, ncclFloat32, 0, comm->comm, rs);
+            if (ne == ncclSuccess && want_srgb)
+                ne = nc.send(root.d->srgb, (size_t)root.rows * row_floats, ncclUint8, 0, comm->comm, rs);
             if (ne == ncclSuccess && is_root)
-                for (uint32_t q = 0; q < n_parts && ne == ncclSuccess; ++q)
-                    ne = nc.recv(r->staging + q * slice, (size_t)part_rows(rows, q, n_parts) * row_floats, ncclFloat32,
-                                 (int)q, comm->comm, rs);
+                for (uint32_t q = 0; q < n_parts && ne == ncclSuccess; ++q) {
+                    const size_t n_q = (size_t)part_rows(rows, q, n_parts) * row_floats;
+                    ne = nc.recv(r->staging + q * slice, n_q, ncclFloat32, (int)q, comm->comm, rs);
+                    if (ne == ncclSuccess && want_srgb)
+                        ne = nc.recv(r->staging_srgb + q * slice, n_q, ncclUint8, (int)q, comm->comm, rs);
+                }
             const ncclResult_t ge = nc.group_end();
             if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
             if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
@@ -739,12 +758,20 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                 r->comm_devices = devs;
             }
             ncclResult_t ne = nc.group_start();
-            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k)
+            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
                 ne = nc.send(parts[k].out_used, (size_t)parts[k].rows * row_floats, ncclFloat32, 0, r->comms[k],
                              parts[k].stream);
-            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k)
+                if (ne == ncclSuccess && want_srgb)
+                    ne = nc.send(parts[k].d->srgb, (size_t)parts[k].rows * row_floats, ncclUint8, 0, r->comms[k],
+                                 parts[k].stream);
+            }
+            for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
                 ne = nc.recv(r->staging + k * slice, (size_t)parts[k].rows * row_floats, ncclFloat32, (int)k,
                              r->comms[0], rs);
+                if (ne == ncclSuccess && want_srgb)
+                    ne = nc.recv(r->staging_srgb + k * slice, (size_t)parts[k].rows * row_floats, ncclUint8, (int)k,
+                                 r->comms[0], rs);
+            }
             const ncclResult_t ge = nc.group_end();
             if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
             if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
@@ -758,18 +785,19 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                 if ((e = hipMemcpyPeerAsync(r->staging + k * slice, root.device, parts[k].out_used, parts[k].device,
                                             (size_t)parts[k].rows * row_floats * sizeof(float), rs)) != hipSuccess)
                     return hip_fail(e, "hipMemcpyPeerAsync");
+                if (want_srgb &&
+                    (e = hipMemcpyPeerAsync(r->staging_srgb + k * slice, root.device, parts[k].d->srgb, parts[k].device,
+                                            (size_t)parts[k].rows * row_floats, rs)) != hipSuccess)
+                    return hip_fail(e, "hipMemcpyPeerAsync srgb");
             }
         }
         if (is_root) {
             float* frame = dev_out ? dev_out : r->full;
             if ((e = rtk_launch_deinterleave(r->staging, slice, frame, rows, W, n_parts, rs)) != hipSuccess)
                 return hip_fail(e, "deinterleave launch");
-            if (host_call && want_srgb && cam->max_depth > 0 &&
-                (e = rtk_launch_to_rgb(frame, r->full_srgb, (uint64_t)rows * row_floats, cam->toon_map, rs)) != hipSuccess)
-                return hip_fail(e, "to_rgb launch");
-            if (host_call && want_srgb && cam->max_depth == 0 &&
-                (e = hipMemsetAsync(r->full_srgb, 0, (size_t)rows * row_floats, rs)) != hipSuccess)
-                return hip_fail(e, "hipMemsetAsync srgb");
+            if (want_srgb &&
+                (e = rtk_launch_deinterleave_u8(r->staging_srgb, slice, r->full_srgb, rows, W, n_parts, rs)) != hipSuccess)
+                return hip_fail(e, "deinterleave launch");
             if ((e = hipEventRecord(r->g_stop, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
             r->g_recorded = true;
         }
