@@ -128,8 +128,9 @@ RTCR_FN bool rounds_ok(double yh, double yl, double err) {
 // sin / cos (k pi/128) from the table: S = sin, C = cos (double-doubles)
 RTCR_FN void sc_table(int k, DD& S, DD& C) {
     const int j = k & 255, q = j >> 6, m = j & 63;
-    const DD t0{RTCR_SIN_PIO128[m][0], RTCR_SIN_PIO128[m][1]};
-    const DD t1{RTCR_SIN_PIO128[64 - m][0], RTCR_SIN_PIO128[64 - m][1]};
+    const double* e = RTCR_SC_PIO128[m];
+    const DD t0{e[0], e[1]};  // sin(m pi/128)
+    const DD t1{e[2], e[3]};  // cos(m pi/128)
     const bool sw = q & 1;
     S = sw ? t1 : t0;
     C = sw ? t0 : t1;
@@ -270,25 +271,28 @@ RTCR_SLOW void sincos_slow(double x, double* s, double* c) {
     *c = yc.h + yc.l;
 }
 
-// A cos r + B sin r (fast path); false when the result's rounding is not certain
+// A cos r + B sin r (fast path); false when the result's rounding is not certain.
+// A + B rh exactly (|A| >= sin(pi/128) > |B rh| unless A = 0), then the
+// small terms, the two largest of them -- A hq = -A rh^2/2 and B t = B (sin r
+// - r) -- last, so that the others round at a finer scale; the bound covers
+// their roundings (2^-53 each) and t's own error (~2^-50.2 relative: r^2 from
+// rh alone, the polynomial, the products) adaptively, everything else stays
+// under 2^-75 |y| or 2^-108 absolute.
 RTCR_FN bool sc_combine(DD A, DD B, double rh, double rl, double hq, double cmr, double t, double& y) {
     RTCR_NOCONTRACT
     const DD b = two_prod(B.h, rh);
-    const DD d = two_prod(A.h, hq);
-    const DD u = two_sum(A.h, b.h);
-    const DD v = two_sum(u.h, d.h);
-    double sm = ((((A.l + u.l) + v.l) + b.l) + d.l);
+    const DD u = fast_two_sum(A.h, b.h);
+    double sm = (A.l + u.l) + b.l;
     sm = fma_(B.h, rl, sm);
     sm = fma_(B.l, rh, sm);
     sm = fma_(A.h, cmr, sm);
     sm = fma_(A.l, hq, sm);
     sm = fma_(B.l, t, sm);
-    const double bt = B.h * t;
-    sm = fma_(B.h, t, sm);  // the largest small term last: the others round at its scale
-    const DD yy = fast_two_sum(v.h, sm);
-    // t carries ~2^-50.2 relative error (r^2 from rh alone, the polynomial's
-    // roundings, the product); everything else < 2^-75 |y| or 2^-108 absolute
-    const double err = fma_(abs_(bt), 0x1p-49, fma_(abs_(yy.h), 0x1p-68, 0x1p-105));
+    const double ah = A.h * hq, bt = B.h * t;
+    sm = fma_(A.h, hq, sm);
+    sm = fma_(B.h, t, sm);
+    const DD yy = fast_two_sum(u.h, sm);
+    const double err = fma_(abs_(bt), 0x1p-49, fma_(abs_(ah), 0x1p-51, fma_(abs_(yy.h), 0x1p-68, 0x1p-105)));
     y = yy.h;
     return rounds_ok(yy.h, yy.l, err);
 }
@@ -305,7 +309,7 @@ RTCR_FN bool sc_prep(double x, ScR& p) {
     const double rh = p.rh;
     const double q2 = rh * rh;
     const double eq = fma_(2.0 * rh, p.rl, fma_(rh, rh, -q2));  // r^2 = q2 + eq
-    const double ps = q2 * (RTCR_S3_H + q2 * (RTCR_S5_H + q2 * (RTCR_S7_H + q2 * RTCR_S9_H)));
+    const double ps = q2 * (RTCR_S3_H + q2 * (RTCR_S5_H + q2 * RTCR_S7_H));  // r^8/9! < 2^-69 r: inside the bound
     p.t = rh * ps;  // sin r - r
     p.hq = -0.5 * q2;
     p.cmr = fma_(q2 * q2, RTCR_C4_H + q2 * (RTCR_C6_H + q2 * RTCR_C8_H), -0.5 * eq);  // cos r - 1 - hq

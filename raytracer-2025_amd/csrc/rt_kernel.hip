@@ -41,6 +41,14 @@ namespace rtk {
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
 #endif
+// Mesh / full tiers: 64-B nodes with 8-bit quantized child boxes (DNode4Q)
+// when the world's bounds allow (rt_render.cpp prepare_tier).  Off: measured
+// slower (A/B at 64 spp, 3 reps, RMSE 0: C4 53.8 -> 57.4 ms, C5 172.4 ->
+// 180.5 ms) -- the decode's ~50 VALU instructions per node visit cost more
+// than the three dwordx4 loads they save.
+#ifndef RT_QNODES
+#define RT_QNODES 0
+#endif
 // Full tier: the same boxed 4-wide nodes, for the walk and the medium boundary walks.
 #ifndef RT_FULL_BVH4
 #define RT_FULL_BVH4 1
@@ -361,13 +369,28 @@ __device__ __forceinline__ bool planar_t_filtered(const SceneView& S, uint32_t i
     return planar_t(S.planars[idx], tri, r, tmin, tmax, t);
 }
 
-// Transform::detransform (shapes.rs:80-84): R^-1 (v - offset) / scale
-__device__ __forceinline__ D3 xf_in(const DXform& X, D3 v) {
-    return mat3(X.rinv, v - d3(X.off[0], X.off[1], X.off[2])) / d3(X.scale[0], X.scale[1], X.scale[2]);
+// Quaternion::rotate_vector (quaternion.rs:72-82): (q * (0, v)) * conj(q)
+// with Mul (quaternion.rs:94-103) term by term in the reference's order; the
+// products with qv.w = 0 are exact zeros, so a + 0*b is a and those terms
+// are left out without changing a bit.
+__device__ __forceinline__ D3 quat_rotate(double w, double x, double y, double z, D3 v) {
+    const double pw = ((-(x * v.x)) - y * v.y) - z * v.z;
+    const double px = (w * v.x + y * v.z) - z * v.y;
+    const double py = (w * v.y - x * v.z) + z * v.x;
+    const double pz = (w * v.z + x * v.y) - y * v.x;
+    const double cx = -x, cy = -y, cz = -z;  // conjugate
+    return d3(((pw * cx + px * w) + py * cz) - pz * cy, ((pw * cy - px * cz) + py * w) + pz * cx,
+              ((pw * cz + px * cy) - py * cx) + pz * w);
 }
-// Transform::transform (shapes.rs:74-78): R (v * scale) + offset
+// Transform::detransform (shapes.rs:80-84): conj(q).rotate_vector(v - offset) / scale
+__device__ __forceinline__ D3 xf_in(const DXform& X, D3 v) {
+    return quat_rotate(X.q[0], -X.q[1], -X.q[2], -X.q[3], v - d3(X.off[0], X.off[1], X.off[2])) /
+           d3(X.scale[0], X.scale[1], X.scale[2]);
+}
+// Transform::transform (shapes.rs:74-78): q.rotate_vector(v * scale) + offset
 __device__ __forceinline__ D3 xf_out(const DXform& X, D3 v) {
-    return mat3(X.rot, v * d3(X.scale[0], X.scale[1], X.scale[2])) + d3(X.off[0], X.off[1], X.off[2]);
+    return quat_rotate(X.q[0], X.q[1], X.q[2], X.q[3], v * d3(X.scale[0], X.scale[1], X.scale[2])) +
+           d3(X.off[0], X.off[1], X.off[2]);
 }
 // shapes.rs:93-99 local ray
 __device__ __forceinline__ Ray xf_ray(const DXform& X, const Ray& r) {
@@ -981,7 +1004,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
         const bool planar = kind == K_TRI || kind == K_QUAD;
         // (the array addresses as values, selected: a select between the
         // SceneView's members made the compiler index a scratch copy of it)
-        const bool qn = S.qnodes != 0;
+        const bool qn = RT_QNODES && S.qnodes != 0;
         const uint64_t a_node = qn ? (uint64_t)S.nodes4q : (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars,
                        a_sphere = (uint64_t)S.spheres;
         uint64_t addr = a_node;
@@ -1268,7 +1291,7 @@ __device__ __forceinline__ uint32_t visit4q_rows(const float4 r0, const float4 r
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
                                                  float c_f, Stack& stk, uint32_t& sp) {
-    if (S.qnodes) {
+    if (RT_QNODES && S.qnodes) {
         const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4q + idx);
         return visit4q_rows(np[0], np[1], np[2], np[3], rf, tmin_f, c_f, stk, sp);
     }
@@ -1467,7 +1490,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
             const DXform& X = S.xforms[h.xf.get(k)];
             rec.p = xf_out(X, rec.p);
             bool ok;
-            rec.n = unit(mat3(X.rot, rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
+            rec.n = unit(quat_rotate(X.q[0], X.q[1], X.q[2], X.q[3], rec.n / d3(X.scale[0], X.scale[1], X.scale[2])), ok);
         }
     }
     if constexpr (PLANAR) {
@@ -2543,6 +2566,7 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 }
 
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
+extern "C" int rtk_qnodes(void) { return RT_QNODES; }
 extern "C" int rtk_planar_filter(void) { return RT_PLANAR_FILTER; }
 extern "C" int rtk_block_threads(int tier) { return tier == rtk::TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }

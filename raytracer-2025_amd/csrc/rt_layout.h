@@ -143,13 +143,14 @@ struct alignas(16) DRemapNM {
     double u_vec[3], v_vec[3];
 };
 
-// Transform (shapes.rs:23-29).  Rotation kept as the quaternion the reference
-// uses plus its 3x3 matrix form (the kernel rotates with the matrix).
+// Transform (shapes.rs:23-29): the quaternion itself -- the kernel rotates
+// with Quaternion::rotate_vector's two products (quaternion.rs:72-103) in the
+// reference's operation order, so a transformed ray has the reference's bits
+// (a 3x3 matrix form is the same rotation but not the same roundings).
 struct alignas(16) DXform {
     double off[3];
     double scale[3];
-    double rot[9];   // R(q), row-major
-    double rinv[9];  // R(conj q)
+    double q[4];  // w, x, y, z
     uint32_t child, pad;
 };
 

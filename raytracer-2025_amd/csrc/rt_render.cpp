@@ -232,9 +232,10 @@ static int prepare_tier(HostWorld& hw) {
             return -1;
         }
     }
-    // mesh / full tiers: 64-B quantized nodes (rt_qnode.h) unless a bound is
-    // not finite (then the 112-B f32 nodes); RT_QNODES=0 keeps f32 nodes (A/B)
-    if (tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
+    // mesh / full tiers of a kernel built with RT_QNODES: 64-B quantized nodes
+    // (rt_qnode.h) unless a bound is not finite (then the 112-B f32 nodes);
+    // RT_QNODES=0 in the environment keeps f32 nodes (A/B)
+    if (rtk_qnodes() && tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
         const char* q = std::getenv("RT_QNODES");
         if (!(q && q[0] == '0')) bvh4_quantize(hw);
     }

@@ -68,14 +68,6 @@ V3 Quat::rotate(V3 v) const {
     return V3(res.x, res.y, res.z);
 }
 
-// 3x3 matrix of v -> q v q* (for the device; the host keeps the quaternion form)
-static void quat_matrix(const Quat& q, double m[9]) {
-    V3 ex = q.rotate(V3(1, 0, 0)), ey = q.rotate(V3(0, 1, 0)), ez = q.rotate(V3(0, 0, 1));
-    m[0] = ex.x; m[1] = ey.x; m[2] = ez.x;
-    m[3] = ex.y; m[4] = ey.y; m[5] = ez.y;
-    m[6] = ex.z; m[7] = ey.z; m[8] = ez.z;
-}
-
 // total_cmp (f64::total_cmp) used by box_compare, bvh.rs:48-54
 static bool total_less(double a, double b) {
     int64_t ia, ib;
@@ -584,8 +576,10 @@ struct Flattener {
                 rtk::DXform x{};
                 x.off[0] = o.offset.x; x.off[1] = o.offset.y; x.off[2] = o.offset.z;
                 x.scale[0] = o.scale.x; x.scale[1] = o.scale.y; x.scale[2] = o.scale.z;
-                quat_matrix(o.q, x.rot);
-                quat_matrix(o.q.conj(), x.rinv);
+                x.q[0] = o.q.w;
+                x.q[1] = o.q.x;
+                x.q[2] = o.q.y;
+                x.q[3] = o.q.z;
                 x.child = C.first;
                 out.xforms.push_back(x);
                 out.features |= rtk::F_XFORM;
