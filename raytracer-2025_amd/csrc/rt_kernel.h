@@ -25,10 +25,20 @@
 // (sphere-count scaling)
 #define RT_NODE_LDS_BYTES 73696
 #endif
+#ifndef RT_MESH_PARK
+// mesh tier: the walk state of lanes whose walk carries over a shading batch
+// is parked in LDS (8 words: 8 KiB per block) across the shading round
+#define RT_MESH_PARK 1
+#endif
 #ifndef RT_STACK_MESH
 // mesh tier: 20 entries = 40 KiB in LDS (4 blocks: the whole 160 KiB), deeper
-// entries in a global overflow column (C4: -1.6 % against 16)
+// entries in a global overflow column (C4: -1.6 % against 16); 16 (32 KiB)
+// with the 8-KiB park area
+#if RT_MESH_PARK
+#define RT_STACK_MESH 16
+#else
 #define RT_STACK_MESH 20
+#endif
 #endif
 #ifndef RT_STACK_FULL
 #define RT_STACK_FULL 16    // full tiers, likewise

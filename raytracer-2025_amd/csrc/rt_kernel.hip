@@ -855,6 +855,36 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     }
 }
 
+// Mesh tier with shading batches (RT_MESH_PARK): the same 8 words; the f32
+// ray, |d|^2 and its reciprocal are made again from the world ray on resume.
+template <class Park>
+__device__ __forceinline__ void trace_park(const Trav<TIER_MESH>& T, Park pk) {
+    constexpr uint32_t B = RT_BLOCK;
+    const uint64_t c = (uint64_t)__double_as_longlong(T.cl.c), ht = (uint64_t)__double_as_longlong(T.hit.t);
+    pk[0 * B] = T.cur;
+    pk[1 * B] = T.sp | ((uint32_t)T.found << 16);
+    pk[2 * B] = (uint32_t)c;
+    pk[3 * B] = (uint32_t)(c >> 32);
+    pk[4 * B] = __float_as_uint(T.cl.c_f);
+    pk[5 * B] = (uint32_t)ht;
+    pk[6 * B] = (uint32_t)(ht >> 32);
+    pk[7 * B] = T.hit.ref;
+}
+template <class Park>
+__device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_MESH>& T, Park pk) {
+    constexpr uint32_t B = RT_BLOCK;
+    T.cur = pk[0 * B];
+    const uint32_t w = pk[1 * B];
+    T.sp = w & 0xffffu;
+    T.found = (w >> 16) & 1u;
+    T.cl.c = __hiloint2double((int)pk[3 * B], (int)pk[2 * B]);
+    T.cl.c_f = __uint_as_float(pk[4 * B]);
+    T.hit.t = __hiloint2double((int)pk[6 * B], (int)pk[5 * B]);
+    T.hit.ref = pk[7 * B];
+    T.rf = make_rayf(wr);
+    T.a = len2(wr.d);
+    T.inva = 1.0 / T.a;
+}
 // Basic tier with shading batches: a carried-over walk's state is parked in
 // LDS across the shading round (the ray-derived fields are made again).
 template <class Park>
@@ -2059,7 +2089,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     // carries over a shading round is parked here across it (RT_PARK_WORDS
     // words: cur, sp | pn | found, c, c_f, hit t, hit ref), so that the
     // shading code does not hold it in registers.
-    constexpr bool PARK = TIER == TIER_BASIC && RT_SHADE_BATCH_BASIC < 64;
+    constexpr bool PARK = (TIER == TIER_BASIC && RT_SHADE_BATCH_BASIC < 64) ||
+                          (TIER == TIER_MESH && RT_MESH_PARK && RT_SHADE_BATCH_MESH < 64);
     __shared__ uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
     RT_LDS uint32_t* pk = (RT_LDS uint32_t*)(park_lds + threadIdx.x);
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
