@@ -59,6 +59,22 @@ def usable_cpus():
     return (min(n, quota) if quota else n), {"affinity": n, "cgroup_quota": quota, "os_cpu_count": os.cpu_count()}
 
 
+def host_topology():
+    """Sockets / cores / threads of the whole host (lscpu), which a GPU box's
+    job only gets a share of."""
+    out = {}
+    try:
+        r = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10)
+        for line in r.stdout.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k in ("CPU(s)", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "Model name"):
+                out[k] = int(v) if v.isdigit() else v
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return out
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -128,7 +144,10 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     scene = rt.Scene(api)
     world, lights, cam, desc = build_workload(scenes, scene, workload, WORKLOADS[workload][0], spp)
     samples, dt = _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads)
+    # one thread on a proportionally sparser sample: the per-core rate
+    samples1, dt1 = _oracle_render(api, capi, scene, world, lights, cam, row_stride * max(1, threads), 1)
     info = cpu_info or {}
+    topo = host_topology()
     res = {
         "value": samples / dt / 1e6,
         "unit": "Msamples/s",
@@ -139,6 +158,21 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
                   f"(all CPUs this job may use: affinity {info.get('affinity')}, cgroup quota {info.get('cgroup_quota')}, "
                   f"os.cpu_count {info.get('os_cpu_count')}; oracle/: reference-semantics C++ restatement, not the Rust binary)",
     }
+    per_core = samples1 / dt1 / 1e6
+    res["per_core"] = {"value": per_core, "unit": "Msamples/s", "seconds": round(dt1, 2), "samples": samples1,
+                       "sample": f"1 thread, every {row_stride * max(1, threads)}th row at {spp} spp"}
+    res["host"] = topo
+    hw_threads = topo.get("CPU(s)") if isinstance(topo.get("CPU(s)"), int) else None
+    if hw_threads:
+        # labelled extrapolation, never the measured baseline: the measured
+        # per-thread rate of the `threads`-thread run times every hardware
+        # thread of the host (linear scaling, as rayon over pixels would
+        # approach on an idle host)
+        res["whole_host_extrapolated"] = {
+            "value": res["value"] / threads * hw_threads, "unit": "Msamples/s", "threads": hw_threads,
+            "basis": f"EXTRAPOLATED, not measured: {res['value']:.3f} Msamples/s on {threads} threads x "
+                     f"{hw_threads}/{threads} ({topo.get('Socket(s)')} sockets x {topo.get('Core(s) per socket')} "
+                     f"cores x {topo.get('Thread(s) per core')} threads)"}
     if workload == "c2":
         s1 = rt.Scene(api)
         w1, l1, cam1 = scenes.random_spheres(s1, 400, 100)

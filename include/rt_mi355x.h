@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum rt_status {
     RT_OK = 0,
@@ -159,6 +159,12 @@ uint32_t rt_camera_image_height(const rt_camera* cam);
 typedef struct rt_comm rt_comm;
 
 typedef struct rt_render_opts {
+    /* sizeof(rt_render_opts) of the caller's header, set by
+     * rt_render_opts_default: the library reads a field only when the
+     * caller's struct holds it, and refuses (RT_EINVAL) a size smaller than
+     * ABI version 3's -- fields are only ever appended. */
+    uint32_t struct_size;
+    uint32_t reserved0;
     uint64_t seed;       /* render RNG key (oracle/rng_contract.hpp) */
     uint32_t row_offset; /* shard: render rows y = row_offset + k*row_stride */
     uint32_t row_stride; /* 0 or 1 = every row */

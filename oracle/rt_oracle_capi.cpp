@@ -416,6 +416,7 @@ uint32_t orc_camera_image_height(const rt_camera* c) {
 }
 void orc_render_opts_default(rt_render_opts* o) {
     std::memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(*o);
     o->seed = 1;
     o->row_stride = 1;
 }

@@ -45,6 +45,8 @@ class RtWorldInfo(C.Structure):
 
 class RtRenderOpts(C.Structure):
     _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("reserved0", C.c_uint32),
         ("seed", C.c_uint64),
         ("row_offset", C.c_uint32),
         ("row_stride", C.c_uint32),

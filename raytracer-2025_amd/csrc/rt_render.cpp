@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <map>
 #include <thread>
 
 #include <rccl/rccl.h>
@@ -189,9 +190,35 @@ static void free_root_buffers(RenderState* r) {
     r->root_device = -1;
 }
 
-static void destroy_comms(RenderState* r) {
-    if (!r->comms.empty() && rccl().ok)
-        for (ncclComm_t c : r->comms) (void)rccl().comm_destroy(c);
+// ncclCommInitAll communicators are process-wide, one set per device list,
+// shared by every scene that renders on that list and kept until the process
+// exits: building a set is slow, and scenes (or calls) that alternate device
+// lists would otherwise rebuild them each time.
+struct CommCache {
+    std::mutex m;
+    std::map<std::vector<int>, std::vector<ncclComm_t>> sets;
+};
+static CommCache& comm_cache() {
+    static CommCache* c = new CommCache();  // never destroyed: RCCL may already be torn down at exit
+    return *c;
+}
+static int32_t nccl_fail(ncclResult_t e, const char* what);
+static int32_t acquire_comms(RenderState* r, const std::vector<int>& devs) {
+    if (r->comm_devices == devs && !r->comms.empty()) return RT_OK;
+    CommCache& cc = comm_cache();
+    std::lock_guard<std::mutex> lk(cc.m);
+    auto it = cc.sets.find(devs);
+    if (it == cc.sets.end()) {
+        std::vector<ncclComm_t> comms(devs.size(), nullptr);
+        const ncclResult_t ne = rccl().comm_init_all(comms.data(), (int)devs.size(), devs.data());
+        if (ne != ncclSuccess) return nccl_fail(ne, "ncclCommInitAll");
+        it = cc.sets.emplace(devs, std::move(comms)).first;
+    }
+    r->comms = it->second;
+    r->comm_devices = devs;
+    return RT_OK;
+}
+static void destroy_comms(RenderState* r) {  // the scene lets go of its cached set
     r->comms.clear();
     r->comm_devices.clear();
 }
@@ -539,12 +566,26 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     // Every stratum row goes out in parts of about RT_PART_SAMPLES (4) samples
     // (rtk_row_parts; decided on the whole frame, so shards and device counts
     // sum rows alike): a launch ends on its longest queue entries.
-    f.parts = rtk_row_parts(f.W, rt_camera_image_height(cam), f.S, env_u32("RT_PART_SAMPLES", 4),
-                            (uint64_t)env_u32("RT_PART_BUDGET_MB", 8192) << 20);
+    // The part-sum buffer is held per scene and device slot (grow-only, freed
+    // with the scene): at most RT_PART_BUDGET_MB (8 GiB) and at most 1/16 of
+    // the device's memory (18 GiB of an MI355X's 288).  A device that cannot
+    // allocate it renders whole rows instead (parts = 1): the same samples,
+    // each row's f64 sum then in one run instead of part sums added in order
+    // (~1 ulp).
+    uint64_t budget = (uint64_t)env_u32("RT_PART_BUDGET_MB", 8192) << 20;
+    size_t mem_free = 0, mem_total = 0;
+    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && mem_total) budget = std::min<uint64_t>(budget, mem_total / 16);
+    f.parts = rtk_row_parts(f.W, rt_camera_image_height(cam), f.S, env_u32("RT_PART_SAMPLES", 4), budget);
     f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
-    if ((rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * f.parts * 3 * sizeof(double),
-                   "hipMalloc partial sums")) != RT_OK)
-        return fail(rc);
+    rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * f.parts * 3 * sizeof(double),
+              "hipMalloc partial sums");
+    if (rc != RT_OK && f.parts > 1) {
+        (void)hipGetLastError();
+        f.parts = 1;
+        rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * 3 * sizeof(double),
+                  "hipMalloc partial sums (whole rows)");
+    }
+    if (rc != RT_OK) return fail(rc);
     if (!p.out &&
         (rc = grow((void**)&d->out, d->out_bytes, (size_t)f.W * f.rows * 3 * sizeof(float), "hipMalloc output")) != RT_OK)
         return fail(rc);
@@ -641,6 +682,10 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                       float* dev_out, bool host_call, bool want_srgb) {
     int32_t rc = validate(s, world, lights, cam);
     if (rc != RT_OK) return rc;
+    if (opts && opts->struct_size < sizeof(rt_render_opts))  // ABI 3 holds every field read below
+        return set_error(RT_EINVAL, "rt_render_opts.struct_size is " + std::to_string(opts->struct_size) +
+                                        ", ABI version 3 needs " + std::to_string(sizeof(rt_render_opts)) +
+                                        ": initialise the options with rt_render_opts_default");
     const uint64_t seed = opts ? opts->seed : 1;
     const uint32_t off = opts ? opts->row_offset : 0;
     const uint32_t stride = (opts && opts->row_stride > 1) ? opts->row_stride : 1;
@@ -701,9 +746,25 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         run_part(s, r, world, lights, cam, seed, reference_bvh, fw, parts[0]);
         for (auto& t : th) t.join();
     }
+    // On any failure after the parts started: wait for the parts that did
+    // enqueue work (their buffers may be reused right away), and leave the
+    // scene in the "nothing rendered" state, not the previous render's.
+    auto abort_render = [&](int32_t code) {
+        const std::string msg = rt_last_error();
+        for (Part& p : parts)
+            if (p.d && p.d->device >= 0 && hipSetDevice(p.d->device) == hipSuccess)
+                (void)hipStreamSynchronize(p.stream);  // own stream, or the caller's (NULL: the default stream)
+        r->n_parts = 0;
+        r->pending = false;
+        r->gathered = false;
+        return set_error(code, msg);
+    };
     double flatten_ms = 0;
     for (Part& p : parts) {
-        if (p.rc != RT_OK) return set_error(p.rc, p.err);
+        if (p.rc != RT_OK) {
+            set_error(p.rc, p.err);
+            return abort_render(p.rc);
+        }
         flatten_ms = std::max(flatten_ms, p.flatten_ms);
     }
     r->n_parts = (int)parts.size();
@@ -718,19 +779,19 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         const size_t slice = (size_t)part_rows(rows, 0, n_parts) * W * 3;  // part 0 has the most rows
         const size_t row_floats = (size_t)W * 3;
         RcclApi& nc = rccl();
-        if ((e = hipSetDevice(root.device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+        if ((e = hipSetDevice(root.device)) != hipSuccess) return abort_render(hip_fail(e, "hipSetDevice"));
         hipStream_t rs = root.stream;
         if (is_root) {
             const size_t full = (dev_out ? 0 : rows * row_floats * sizeof(float));
             const size_t srgb = want_srgb ? rows * row_floats : 0;
-            if ((rc = root_buffers(r, root.device, n_parts * slice * sizeof(float), full, srgb)) != RT_OK) return rc;
-            if ((e = hipEventRecord(r->g_start, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+            if ((rc = root_buffers(r, root.device, n_parts * slice * sizeof(float), full, srgb)) != RT_OK) return abort_render(rc);
+            if ((e = hipEventRecord(r->g_start, rs)) != hipSuccess) return abort_render(hip_fail(e, "hipEventRecord"));
         }
         bool distinct = true;
         for (uint32_t i = 0; i < nd && !comm; ++i)
             for (uint32_t j = i + 1; j < nd; ++j) distinct = distinct && opts->devices[i] != opts->devices[j];
         if (comm) {
-            if (!nc.ok) return set_error(RT_EDEVICE, nc.err);
+            if (!nc.ok) return abort_render(set_error(RT_EDEVICE, nc.err));
             ncclResult_t ne = nc.group_start();
             if (ne == ncclSuccess)
                 ne = nc.send(root.out_used, (size_t)root.rows * row_floats, ncclFloat32, 0, comm->comm, rs);
@@ -744,20 +805,11 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                         ne = nc.recv(r->staging_srgb + q * slice, n_q, ncclUint8, (int)q, comm->comm, rs);
                 }
             const ncclResult_t ge = nc.group_end();
-            if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
-            if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+            if (ne != ncclSuccess) return abort_render(nccl_fail(ne, "ncclSend/ncclRecv"));
+            if (ge != ncclSuccess) return abort_render(nccl_fail(ge, "ncclGroupEnd"));
         } else if (distinct && nc.ok) {
-            std::vector<int> devs(opts->devices, opts->devices + nd);
-            if (r->comm_devices != devs) {
-                destroy_comms(r);
-                r->comms.assign(nd, nullptr);
-                ncclResult_t ne = nc.comm_init_all(r->comms.data(), (int)nd, devs.data());
-                if (ne != ncclSuccess) {
-                    r->comms.clear();
-                    return nccl_fail(ne, "ncclCommInitAll");
-                }
-                r->comm_devices = devs;
-            }
+            const std::vector<int> devs(opts->devices, opts->devices + nd);
+            if ((rc = acquire_comms(r, devs)) != RT_OK) return abort_render(rc);
             ncclResult_t ne = nc.group_start();
             for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
                 ne = nc.send(parts[k].out_used, (size_t)parts[k].rows * row_floats, ncclFloat32, 0, r->comms[k],
@@ -774,36 +826,36 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                                  r->comms[0], rs);
             }
             const ncclResult_t ge = nc.group_end();
-            if (ne != ncclSuccess) return nccl_fail(ne, "ncclSend/ncclRecv");
-            if (ge != ncclSuccess) return nccl_fail(ge, "ncclGroupEnd");
+            if (ne != ncclSuccess) return abort_render(nccl_fail(ne, "ncclSend/ncclRecv"));
+            if (ge != ncclSuccess) return abort_render(nccl_fail(ge, "ncclGroupEnd"));
         } else {
             // a device listed twice (one communicator per device is all RCCL
             // allows) or no librccl: peer copies onto the root
             for (uint32_t k = 0; k < nd; ++k) {
                 if (!parts[k].rows) continue;
                 if ((e = hipStreamWaitEvent(rs, parts[k].d->ev_done, 0)) != hipSuccess)
-                    return hip_fail(e, "hipStreamWaitEvent");
+                    return abort_render(hip_fail(e, "hipStreamWaitEvent"));
                 if ((e = hipMemcpyPeerAsync(r->staging + k * slice, root.device, parts[k].out_used, parts[k].device,
                                             (size_t)parts[k].rows * row_floats * sizeof(float), rs)) != hipSuccess)
-                    return hip_fail(e, "hipMemcpyPeerAsync");
+                    return abort_render(hip_fail(e, "hipMemcpyPeerAsync"));
                 if (want_srgb &&
                     (e = hipMemcpyPeerAsync(r->staging_srgb + k * slice, root.device, parts[k].d->srgb, parts[k].device,
                                             (size_t)parts[k].rows * row_floats, rs)) != hipSuccess)
-                    return hip_fail(e, "hipMemcpyPeerAsync srgb");
+                    return abort_render(hip_fail(e, "hipMemcpyPeerAsync srgb"));
             }
         }
         if (is_root) {
             float* frame = dev_out ? dev_out : r->full;
             if ((e = rtk_launch_deinterleave(r->staging, slice, frame, rows, W, n_parts, rs)) != hipSuccess)
-                return hip_fail(e, "deinterleave launch");
+                return abort_render(hip_fail(e, "deinterleave launch"));
             if (want_srgb &&
                 (e = rtk_launch_deinterleave_u8(r->staging_srgb, slice, r->full_srgb, rows, W, n_parts, rs)) != hipSuccess)
-                return hip_fail(e, "deinterleave launch");
-            if ((e = hipEventRecord(r->g_stop, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+                return abort_render(hip_fail(e, "deinterleave launch"));
+            if ((e = hipEventRecord(r->g_stop, rs)) != hipSuccess) return abort_render(hip_fail(e, "hipEventRecord"));
             r->g_recorded = true;
         }
         // the root's slot is reused only after the gather read it
-        if ((e = hipEventRecord(root.d->ev_done, rs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+        if ((e = hipEventRecord(root.d->ev_done, rs)) != hipSuccess) return abort_render(hip_fail(e, "hipEventRecord"));
     }
     r->pending = true;
     return RT_OK;

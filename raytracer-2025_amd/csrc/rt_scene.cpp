@@ -1252,6 +1252,7 @@ uint32_t rt_camera_image_height(const rt_camera* c) {
 void rt_render_opts_default(rt_render_opts* o) {
     if (!o) return;
     std::memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(*o);
     o->seed = 1;
     o->row_stride = 1;
 }

@@ -130,3 +130,18 @@ def test_comm_and_partials_without_render(product, rt):
     assert not product.comm_init(uid, 2, 5)  # rank out of range
     s = rt.Scene(product)
     assert product.render_partials_get(s.s, None, 0) == -1
+
+
+def test_render_opts_struct_size_checked(product, rt, scenes, capi):
+    """rt_render_opts carries its size (ABI 3): options not made by
+    rt_render_opts_default (struct_size 0, an older and smaller struct) are
+    refused before anything is read past the caller's struct."""
+    s = rt.Scene(product)
+    world, lights, cam = scenes.random_spheres(s, 8, 1)
+    opts = capi.RtRenderOpts()
+    product.render_opts_default(ctypes.byref(opts))
+    assert opts.struct_size == ctypes.sizeof(capi.RtRenderOpts) and product.abi_version() == 3
+    opts.struct_size = 0
+    c = cam.to_c()
+    assert product.render(s.s, world.h, -1, ctypes.byref(c), ctypes.byref(opts), None, None, None) == -1
+    assert b"struct_size" in product.last_error()
