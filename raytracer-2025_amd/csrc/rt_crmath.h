@@ -16,7 +16,8 @@
 // double-double arithmetic to ~2^-100 and rounds that.  Reductions:
 //   sin / cos: x = k pi/128 + r, |r| <= pi/256 (Cody-Waite with a 26-bit first
 //     constant below 2^20, Payne-Hanek with the 128/pi bits above), then
-//     sin x = S cos r + C sin r with S, C = sin / cos(k pi/128) from a table.
+//     sin x = S cos r + C sin r with S, C = sin / cos(k pi/128) from a
+//     256-record table (8 KiB, L1-resident).
 //   log: x = 2^e z, r = z c - 1 exact as a double-double (|r| < 2^-7), then
 //     log x = e ln2 - log c + log1p(r); c = 1 around 1, so log x near 1 is
 //     log1p(r) without cancellation.
@@ -127,15 +128,9 @@ RTCR_FN bool rounds_ok(double yh, double yl, double err) {
 // ------------------------------------------------------------------ sin / cos
 // sin / cos (k pi/128) from the table: S = sin, C = cos (double-doubles)
 RTCR_FN void sc_table(int k, DD& S, DD& C) {
-    const int j = k & 255, q = j >> 6, m = j & 63;
-    const double* e = RTCR_SC_PIO128[m];
-    const DD t0{e[0], e[1]};  // sin(m pi/128)
-    const DD t1{e[2], e[3]};  // cos(m pi/128)
-    const bool sw = q & 1;
-    S = sw ? t1 : t0;
-    C = sw ? t0 : t1;
-    if (q >= 2) S = dd_neg(S);
-    if ((q + 1) & 2) C = dd_neg(C);
+    const double* e = RTCR_SC_PIO128[k & 255];  // one 32-B record: no quadrant folding
+    S = DD{e[0], e[1]};
+    C = DD{e[2], e[3]};
 }
 
 // |x| <= 2^20: x = k pi/128 + (rh + rl), |error| < 2^-108
