@@ -7,8 +7,7 @@
 // the format is HDR / EXR / AVIF, converts RGB with palette's sRGB EOTF
 // (utils/image.rs:21-82).  This restates that pipeline for PNG -- the only
 // image format among the reference's assets besides one JPEG -- over zlib's
-// inflate.  Interlaced PNGs and other formats are reported as unsupported
-// (the reference would decode them), never read as something else.
+// inflate, interlaced (Adam7) or not.
 // tests/test_png_cpu.py pins the decoder against PIL on the reference's own
 // PNG assets (8-bit RGB / RGBA / gray, 4-bit palette) and on synthetic files
 // covering every color type, bit depth and filter.
@@ -76,9 +75,9 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
         err = "PNG without IHDR / IDAT";
         return CORRUPT;
     }
-    if (interlace) {
-        err = "interlaced PNG (Adam7) is not decoded here";
-        return UNSUPPORTED;
+    if (interlace > 1) {
+        err = "bad PNG interlace method";
+        return CORRUPT;
     }
     int channels;
     switch (ctype) {
@@ -101,34 +100,25 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
         return UNSUPPORTED;
     }
     const size_t bpp_bits = (size_t)channels * depth;
-    const size_t stride = ((size_t)W * bpp_bits + 7) / 8;
     const size_t bpp = std::max<size_t>(1, bpp_bits / 8);  // filter byte distance
-    std::vector<uint8_t> raw((stride + 1) * H);
+    // the passes: the whole image, or Adam7's seven (x0, y0, dx, dy) sub-images,
+    // each its own run of filtered scanlines
+    static const uint32_t ADAM7[7][4] = {{0, 0, 8, 8}, {4, 0, 8, 8}, {0, 4, 4, 8}, {2, 0, 4, 4},
+                                         {0, 2, 2, 4}, {1, 0, 2, 2}, {0, 1, 1, 2}};
+    static const uint32_t WHOLE[1][4] = {{0, 0, 1, 1}};
+    const uint32_t (*passes)[4] = interlace ? ADAM7 : WHOLE;
+    const int n_pass = interlace ? 7 : 1;
+    size_t raw_size = 0;
+    for (int k = 0; k < n_pass; ++k) {
+        const uint32_t pw = (W - passes[k][0] + passes[k][2] - 1) / passes[k][2];
+        const uint32_t ph = (H - passes[k][1] + passes[k][3] - 1) / passes[k][3];
+        if (W > passes[k][0] && H > passes[k][1] && pw && ph) raw_size += ((pw * bpp_bits + 7) / 8 + 1) * (size_t)ph;
+    }
+    std::vector<uint8_t> raw(raw_size);
     uLongf out_len = (uLongf)raw.size();
     if (uncompress(raw.data(), &out_len, idat.data(), (uLong)idat.size()) != Z_OK || out_len != raw.size()) {
         err = "PNG zlib stream does not inflate to the image size";
         return CORRUPT;
-    }
-    // unfilter in place (filter types 0-4)
-    std::vector<uint8_t> img(stride * H);
-    for (uint32_t y = 0; y < H; ++y) {
-        const uint8_t ft = raw[y * (stride + 1)];
-        const uint8_t* src = &raw[y * (stride + 1) + 1];
-        uint8_t* cur = &img[y * stride];
-        const uint8_t* prev = y ? &img[(y - 1) * stride] : nullptr;
-        for (size_t i = 0; i < stride; ++i) {
-            const int a = i >= bpp ? cur[i - bpp] : 0, b = prev ? prev[i] : 0, c = (prev && i >= bpp) ? prev[i - bpp] : 0;
-            int v = src[i];
-            switch (ft) {
-                case 0: break;
-                case 1: v += a; break;
-                case 2: v += b; break;
-                case 3: v += (a + b) >> 1; break;
-                case 4: v += paeth(a, b, c); break;
-                default: err = "bad PNG filter type"; return CORRUPT;
-            }
-            cur[i] = (uint8_t)v;
-        }
     }
     rgba.assign((size_t)W * H * 4, 1.0f);
     const float max_v = depth == 16 ? 65535.0f : 255.0f;
@@ -138,33 +128,63 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
         const size_t bit = idx * depth;
         return (row[bit / 8] >> (8 - depth - bit % 8)) & ((1u << depth) - 1);
     };
-    for (uint32_t y = 0; y < H; ++y) {
-        const uint8_t* row = &img[y * stride];
-        for (uint32_t x = 0; x < W; ++x) {
-            float* o = &rgba[((size_t)y * W + x) * 4];
-            if (ctype == 3) {
-                const uint32_t k = sample(row, x);
-                if (3 * k + 2 >= plte.size()) {
-                    err = "PNG palette index out of range";
-                    return CORRUPT;
+    size_t at = 0;
+    for (int k = 0; k < n_pass; ++k) {
+        const uint32_t x0 = passes[k][0], y0 = passes[k][1], dx = passes[k][2], dy = passes[k][3];
+        if (W <= x0 || H <= y0) continue;
+        const uint32_t pw = (W - x0 + dx - 1) / dx, ph = (H - y0 + dy - 1) / dy;
+        const size_t stride = ((size_t)pw * bpp_bits + 7) / 8;
+        // unfilter the pass (filter types 0-4), each row against the pass's previous row
+        std::vector<uint8_t> img(stride * ph);
+        for (uint32_t y = 0; y < ph; ++y) {
+            const uint8_t ft = raw[at + y * (stride + 1)];
+            const uint8_t* src = &raw[at + y * (stride + 1) + 1];
+            uint8_t* cur = &img[y * stride];
+            const uint8_t* prev = y ? &img[(y - 1) * stride] : nullptr;
+            for (size_t i = 0; i < stride; ++i) {
+                const int a = i >= bpp ? cur[i - bpp] : 0, b = prev ? prev[i] : 0,
+                          c = (prev && i >= bpp) ? prev[i - bpp] : 0;
+                int v = src[i];
+                switch (ft) {
+                    case 0: break;
+                    case 1: v += a; break;
+                    case 2: v += b; break;
+                    case 3: v += (a + b) >> 1; break;
+                    case 4: v += paeth(a, b, c); break;
+                    default: err = "bad PNG filter type"; return CORRUPT;
                 }
-                for (int c = 0; c < 3; ++c) o[c] = (float)plte[3 * k + c] / 255.0f;
-                o[3] = k < trns.size() ? (float)trns[k] / 255.0f : 1.0f;
-            } else if (ctype == 0 || ctype == 4) {
-                const uint32_t g = sample(row, (size_t)x * channels);
-                // sub-8-bit gray is scaled to 8 bits first (the png crate's EXPAND)
-                const float gv = depth < 8 ? (float)(g * 255u / ((1u << depth) - 1)) / 255.0f : (float)g / max_v;
-                o[0] = o[1] = o[2] = gv;
-                if (ctype == 4) o[3] = (float)sample(row, (size_t)x * 2 + 1) / max_v;
-                else if (trns.size() >= 2 && g == ((uint32_t)trns[0] << 8 | trns[1])) o[3] = 0.0f;
-            } else {
-                uint32_t v[4];
-                for (int c = 0; c < channels; ++c) v[c] = sample(row, (size_t)x * channels + c);
-                for (int c = 0; c < 3; ++c) o[c] = (float)v[c] / max_v;
-                if (ctype == 6) o[3] = (float)v[3] / max_v;
-                else if (trns.size() >= 6 && v[0] == ((uint32_t)trns[0] << 8 | trns[1]) &&
-                         v[1] == ((uint32_t)trns[2] << 8 | trns[3]) && v[2] == ((uint32_t)trns[4] << 8 | trns[5]))
-                    o[3] = 0.0f;
+                cur[i] = (uint8_t)v;
+            }
+        }
+        at += (stride + 1) * ph;
+        for (uint32_t y = 0; y < ph; ++y) {
+            const uint8_t* row = &img[y * stride];
+            for (uint32_t x = 0; x < pw; ++x) {
+                float* o = &rgba[((size_t)(y0 + y * dy) * W + (x0 + x * dx)) * 4];
+                if (ctype == 3) {
+                    const uint32_t kk = sample(row, x);
+                    if (3 * kk + 2 >= plte.size()) {
+                        err = "PNG palette index out of range";
+                        return CORRUPT;
+                    }
+                    for (int c = 0; c < 3; ++c) o[c] = (float)plte[3 * kk + c] / 255.0f;
+                    o[3] = kk < trns.size() ? (float)trns[kk] / 255.0f : 1.0f;
+                } else if (ctype == 0 || ctype == 4) {
+                    const uint32_t g = sample(row, (size_t)x * channels);
+                    // sub-8-bit gray is scaled to 8 bits first (the png crate's EXPAND)
+                    const float gv = depth < 8 ? (float)(g * 255u / ((1u << depth) - 1)) / 255.0f : (float)g / max_v;
+                    o[0] = o[1] = o[2] = gv;
+                    if (ctype == 4) o[3] = (float)sample(row, (size_t)x * 2 + 1) / max_v;
+                    else if (trns.size() >= 2 && g == ((uint32_t)trns[0] << 8 | trns[1])) o[3] = 0.0f;
+                } else {
+                    uint32_t v[4];
+                    for (int c = 0; c < channels; ++c) v[c] = sample(row, (size_t)x * channels + c);
+                    for (int c = 0; c < 3; ++c) o[c] = (float)v[c] / max_v;
+                    if (ctype == 6) o[3] = (float)v[3] / max_v;
+                    else if (trns.size() >= 6 && v[0] == ((uint32_t)trns[0] << 8 | trns[1]) &&
+                             v[1] == ((uint32_t)trns[2] << 8 | trns[3]) && v[2] == ((uint32_t)trns[4] << 8 | trns[5]))
+                        o[3] = 0.0f;
+                }
             }
         }
     }

@@ -4,8 +4,12 @@ into_rgba32f (8-bit v / 255, 16-bit v / 65535, gray -> (g, g, g), palette +
 tRNS -> RGBA) on the reference's own PNG assets read in place (4-bit palette,
 8-bit gray, RGB, RGBA) and on synthetic files of every color type / bit depth
 PIL writes; then palette's sRGB EOTF in f32 (utils/image.rs:63-82) against
-the formula in numpy.  A missing file is Image::EMPTY; JPEG and interlaced
-PNG are reported unsupported (never read as something else)."""
+the formula in numpy.  Interlaced (Adam7) files are written by the test
+itself (PIL reads them but does not write them) with every filter type.  A
+missing file is Image::EMPTY; JPEG is reported unsupported (never read as
+something else)."""
+import struct
+import zlib
 import os
 import subprocess
 
@@ -100,8 +104,93 @@ def test_missing_and_unsupported(dump, tmp_path):
     assert dump(str(tmp_path / "broken.png"), False, tmp_path)[0] == 1  # decode error -> EMPTY, as the reference
     PIL.new("RGB", (8, 8)).save(str(tmp_path / "x.jpg"))
     assert dump(str(tmp_path / "x.jpg"), False, tmp_path)[0] == 3
-    PIL.new("RGB", (9, 9), (10, 20, 30)).save(str(tmp_path / "il.png"), interlace=1)
-    st, px = dump(str(tmp_path / "il.png"), False, tmp_path)
-    assert st in (0, 3)  # PIL may not interlace; an interlaced file is reported, never misread
-    if st == 0:
-        np.testing.assert_array_equal(px[..., :3], srgb_to_linear(pil_rgba01(str(tmp_path / "il.png"))[..., :3]))
+
+
+ADAM7 = [(0, 0, 8, 8), (4, 0, 8, 8), (0, 4, 4, 8), (2, 0, 4, 4), (0, 2, 2, 4), (1, 0, 2, 2), (0, 1, 1, 2)]
+
+
+def _pack_row(samples, depth):
+    """One scanline's samples (uint array) packed at `depth` bits, big-endian."""
+    if depth == 16:
+        return samples.astype(">u2").tobytes()
+    if depth == 8:
+        return samples.astype(np.uint8).tobytes()
+    bits = np.zeros(len(samples) * depth, dtype=np.uint8)
+    for b in range(depth):
+        bits[b::depth] = (samples >> (depth - 1 - b)) & 1
+    return np.packbits(bits).tobytes()
+
+
+def _filter(row, prev, bpp, ft):
+    out = bytearray(len(row))
+    for i in range(len(row)):
+        a = row[i - bpp] if i >= bpp else 0
+        b = prev[i] if prev is not None else 0
+        c = prev[i - bpp] if (prev is not None and i >= bpp) else 0
+        if ft == 0:
+            pred = 0
+        elif ft == 1:
+            pred = a
+        elif ft == 2:
+            pred = b
+        elif ft == 3:
+            pred = (a + b) >> 1
+        else:
+            p = a + b - c
+            pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
+            pred = a if (pa <= pb and pa <= pc) else (b if pb <= pc else c)
+        out[i] = (row[i] - pred) & 255
+    return bytes(out)
+
+
+def write_adam7_png(path, img, ctype, depth, rng, plte=None):
+    """img: (h, w, channels) uint array; every pass row gets a random filter type."""
+    h, w, ch = img.shape
+    bpp = max(1, ch * depth // 8)
+    data = bytearray()
+    for x0, y0, dx, dy in ADAM7:
+        sub = img[y0::dy, x0::dx]
+        if sub.shape[0] == 0 or sub.shape[1] == 0:
+            continue
+        prev = None
+        for r in sub:
+            row = _pack_row(r.reshape(-1), depth)
+            ft = int(rng.integers(0, 5))
+            data += bytes([ft]) + _filter(row, prev, bpp, ft)
+            prev = row
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    png = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 1))
+    if plte is not None:
+        png += chunk(b"PLTE", plte)
+    png += chunk(b"IDAT", zlib.compress(bytes(data))) + chunk(b"IEND", b"")
+    with open(path, "wb") as f:
+        f.write(png)
+
+
+@pytest.mark.parametrize("kind", ["rgb8", "rgba16", "gray1", "gray4", "gray16", "palette2", "la8"])
+@pytest.mark.parametrize("size", [(1, 1), (5, 3), (9, 9), (37, 23)])
+def test_interlaced_adam7_matches_pil(dump, tmp_path, kind, size):
+    """Adam7 (PNG 1.2 section 8): seven sub-images, each its own filtered
+    scanlines, scattered back onto the grid -- against PIL's decoding."""
+    rng = np.random.default_rng(sum(map(ord, kind)) + size[0])
+    w, h = size
+    ctype, depth, ch = {"rgb8": (2, 8, 3), "rgba16": (6, 16, 4), "gray1": (0, 1, 1), "gray4": (0, 4, 1),
+                        "gray16": (0, 16, 1), "palette2": (3, 2, 1), "la8": (4, 8, 2)}[kind]
+    img = rng.integers(0, 1 << depth, size=(h, w, ch), dtype=np.uint32)
+    plte = bytes(rng.integers(0, 256, size=12, dtype=np.uint8)) if ctype == 3 else None
+    path = str(tmp_path / f"a7_{kind}.png")
+    write_adam7_png(path, img, ctype, depth, rng, plte)
+    st, px = dump(path, True, tmp_path)
+    assert st == 0
+    if depth == 16 and ctype in (2, 4, 6):
+        # PIL keeps 8 bits of 16-bit color; into_rgba32f is v / 65535: check
+        # the grid against PIL's high bytes and the values against the samples
+        np.testing.assert_array_equal(np.round(px * 65535).astype(np.uint32) >> 8,
+                                      np.round(pil_rgba01(path) * 255).astype(np.uint32))
+        exp = img.astype(np.float32) / np.float32(65535)
+        if ch == 4:
+            np.testing.assert_array_equal(px, exp)
+    else:
+        np.testing.assert_array_equal(px, pil_rgba01(path))
