@@ -11,7 +11,7 @@
 
 #include "../include/rt_mi355x.h"
 #include "rt_oracle.hpp"
-#include "../raytracer-2025_amd/csrc/rt_png.hpp"
+#include "orc_png.hpp"
 
 using namespace orc;
 
@@ -94,14 +94,24 @@ int32_t orc_tex_image(rt_scene* s, uint32_t w, uint32_t h, const float* rgba, in
     s->tex.push_back(t);
     return (int32_t)s->tex.size() - 1;
 }
-// ImageTexture::new / new_raw_image from a file (test tooling shares the
-// library's PNG decoder, rt_png.hpp, pinned against PIL by tests/test_png_cpu.py)
+// Image::new(path, raw) + pixel_data's colour handling (utils/image.rs:21-82)
+// with the oracle's own PNG reader (orc_png.hpp): a file that cannot be
+// opened or decoded is Image::EMPTY (0 x 0: cyan), a file that is not a PNG
+// is refused (the product library refuses it too: RT_EUNSUPPORTED).
+static bool orc_load_image(const std::string& path, bool raw, uint32_t& w, uint32_t& h, std::vector<float>& px) {
+    const orcpng::Result r = orcpng::decode_file(path, w, h, px);
+    if (r == orcpng::NOT_PNG) return false;
+    if (r == orcpng::DECODED && !raw)
+        for (size_t i = 0; i < px.size(); i += 4)
+            for (int c = 0; c < 3; ++c) px[i + c] = orcpng::eotf(px[i + c]);
+    return true;
+}
+// ImageTexture::new / new_raw_image from a file
 int32_t orc_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t linear) {
     if (!s || !path) return fail(RT_EINVAL, "null");
     uint32_t w = 0, h = 0;
     std::vector<float> px;
-    std::string err;
-    if (rtpng::load(path, raw != 0, w, h, px, err) == rtpng::UNSUPPORTED) return fail(RT_EUNSUPPORTED, err);
+    if (!orc_load_image(path, raw != 0, w, h, px)) return fail(RT_EUNSUPPORTED, std::string(path) + ": not a PNG");
     return orc_tex_image(s, w, h, px.empty() ? nullptr : px.data(), linear);
 }
 int32_t orc_tex_noise(rt_scene* s, double scale, uint64_t seed) {
@@ -270,7 +280,10 @@ int32_t orc_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
     auto image = [&](const std::string& file, bool raw) -> std::shared_ptr<ImageTexture> {
         auto t = std::make_shared<ImageTexture>();
         uint32_t w = 0, h = 0;
-        if (rtpng::load(prefix + "/" + file, raw, w, h, t->rgba, img_err) == rtpng::UNSUPPORTED) return nullptr;
+        if (!orc_load_image(prefix + "/" + file, raw, w, h, t->rgba)) {
+            img_err = prefix + "/" + file + ": not a PNG";
+            return nullptr;
+        }
         t->w = (int)w;
         t->h = (int)h;  // 0 x 0: missing -> cyan (texture.rs:167-169)
         t->linear_interp = raw;

@@ -23,12 +23,15 @@ REF_ASSETS = "/root/reference/assets/Final"
 PIL = pytest.importorskip("PIL.Image")
 
 
-@pytest.fixture(scope="module")
-def dump():
+@pytest.fixture(scope="module", params=["product", "oracle"])
+def dump(request):
+    """The library's decoder (rt_png.hpp) and, independently written, the
+    oracle's (oracle/orc_png.hpp): both against PIL."""
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "png_dump.%d" % os.getpid())  # one per pytest worker
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", os.path.join(HERE, "cpp", "png_dump.cpp"), "-o",
-                    exe, "-lz"], check=True)
+    exe = os.path.join(BUILD, "png_dump_%s.%d" % (request.param, os.getpid()))  # one per pytest worker
+    flags = ["-DORACLE_PNG"] if request.param == "oracle" else []
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", *flags, os.path.join(HERE, "cpp", "png_dump.cpp"),
+                    "-o", exe, "-lz"], check=True)
 
     def run(path, raw, tmp):
         out = os.path.join(str(tmp), "dump.bin")
