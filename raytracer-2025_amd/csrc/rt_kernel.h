@@ -86,10 +86,12 @@ struct rtk_frame_desc {
     uint32_t S, max_depth;
     uint64_t seed;
     uint32_t defocus, pad;
-    // every stratum row is traced in `parts` queue entries of consecutive
-    // samples (rtk::Frame::parts; rtk_row_parts), summed in part order
+    // the stratum rows of the shard's first whole_rows rows are one queue
+    // entry each; every later row is `parts` entries of consecutive samples
+    // (rtk::Frame; rtk_row_parts, rtk_tail_rows), summed in part order
     uint32_t parts;
     uint32_t chunk_min;  // smallest guided chunk of queue entries (0: what the wave needs)
+    uint32_t whole_rows, pad2;
 
     double recip_sqrt_spp, pixel_sample_scale;
     double center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3];
@@ -111,11 +113,17 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
                                        double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
                                        int toon, hipStream_t stream, int tier, int grid, void* params_dev,
                                        void* stack_ovf);
-// Queue entries per stratum row for a W x H frame at S x S samples: parts of
-// about part_samples samples (0: whole rows), as many as keep the part sums
-// of the WHOLE frame within budget_bytes.  A function of the frame only, not
-// of a shard, so every row shard and device count sums a row the same way.
-extern "C" uint32_t rtk_row_parts(uint32_t W, uint32_t H, uint32_t S, uint32_t part_samples, uint64_t budget_bytes);
+// Queue entries per tail stratum row at S x S samples: parts of about
+// part_samples samples (0: whole rows), none empty.
+extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples);
+// The tail of a W x H frame: its last image rows whose stratum rows go out in
+// `parts` entries -- about permille / 1000 of H, fewer when the tail's extra
+// part sums (parts - 1 per stratum row, 24 B each) would pass budget_bytes or
+// the frame's queue 2^32 entries.  A function of the frame only, not of a
+// shard, so every row shard and device count sums a row the same way; each
+// shard's tail rows are its last rows, so every shard ends on short entries.
+extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint64_t budget_bytes,
+                                  uint32_t permille);
 // Re-interleaves a gathered frame: staging holds `parts` slices of `slice`
 // floats, slice k = the compact rows k, k + parts, ... of the frame; out gets
 // the frame's `rows` compact rows (rows x W x 3 f32).

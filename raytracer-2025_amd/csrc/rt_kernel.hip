@@ -91,21 +91,24 @@ struct Frame {
     uint32_t max_depth;
     uint32_t key0, key1;
     uint32_t total_items;
-    // Work queue: entry q = part q % parts of stratum row q / parts (item =
-    // launch pixel * S + s_i); a part traces part_len consecutive samples s_j
-    // (the last part the rest) and writes their f64 sum to partial slot
-    // (s_i * parts + part) * pixels + pixel -- pixel-minor, so that the
-    // reduce reads coalesced -- and the reduce adds a row's parts in order.
-    // A launch ends on its longest queue entries, and a whole row of a pixel
-    // whose paths bounce 40 times inside a glass sphere is ~10 ms of one wave
-    // (scripts/lane_trace.py): parts keep the last entries short.
-    uint32_t parts, part_len, queue_total;
+    // Work queue (item = launch pixel * S + s_i, a stratum row): the shard's
+    // first whole_items items -- the pixels of its rows above the frame's
+    // tail rows (rtk_tail_rows) -- are one entry each, a whole row of S
+    // samples; every later item is `parts` entries of part_len consecutive
+    // samples s_j (the last part the rest), so that the last entries of a
+    // launch are short: a whole row of a pixel whose paths bounce 40 times
+    // inside a glass sphere is ~10 ms of one wave (scripts/lane_trace.py).
+    // Entry q writes its f64 sum to partial slot q (queue order: the lanes
+    // of a wave take consecutive entries, so their 24-B sums fill whole L2
+    // lines), and the reduce adds a tail row's parts in part order.
+    uint32_t parts, part_len, queue_total, whole_items;
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
     // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
     // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
     double inv_parts, inv_S, inv_W;
     float inv_guide;
+    float parts_m1, inv_parts_f;  // parts - 1 and 1 / parts: the guided chunk in part-sized entries
     uint32_t defocus;
     double recip_sqrt_spp, pixel_sample_scale;
     D3 center, pixel00, du, dv, disk_u, disk_v;
@@ -2175,10 +2178,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             uint32_t chunk = RT_QUEUE_CHUNK;
 #if RT_QUEUE_GUIDE
             {
+                // the work left in part-sized entries (a whole-row entry is
+                // `parts` of them), and the chunk in the entries it takes: a
+                // pool of whole rows taken as the tail starts is no larger
+                // in samples than the tail's pools (it would outlast them)
                 const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
-                const uint32_t g = max((uint32_t)((float)left * F.inv_guide), F.chunk_min);
+                const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
                 constexpr uint32_t CAP = TIER == TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK;
-                chunk = max(min(g, CAP), avail < n ? n - avail : 0u);
+                const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
+                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), CAP);
+                chunk = max(max(chunk, F.chunk_min), avail < n ? n - avail : 0u);
             }
 #endif
             if (avail < n) {
@@ -2211,12 +2220,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_steps_q = trace_steps;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                const uint32_t item = udiv_inv(q, F.inv_parts), part = q - item * F.parts;
-                s_j = part * F.part_len;
+                const bool whole = q < F.whole_items;
+                const uint32_t qt = q - F.whole_items, it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
+                const uint32_t item = whole ? q : F.whole_items + it;
+                s_j = whole ? 0u : part * F.part_len;
                 acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
-                sie = s_i | (min(F.S, s_j + F.part_len) << 16);
-                slot = (s_i * F.parts + part) * (F.W * F.rows) + pl;
+                sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
+                slot = q;
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
             }
@@ -2481,26 +2492,29 @@ __device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
     return (uint8_t)(q < 0.0 ? 0.0 : (q > 255.0 ? 255.0 : q));
 }
 
-// Sums the S stratum rows of each pixel in s_i order -- a row = its `parts`
-// part sums added in part order; slot (s_i * parts + part) * npix + pixel,
-// so a wave's loads are coalesced -- * pixel_sample_scale,
-// to linear f32 (camera.rs:193), and -- when srgb is given -- the pixel's
-// to_rgb bytes from the f64 sum, as the reference converts its f64 color.
+// Sums the S stratum rows of each pixel in s_i order -- a row = its one
+// whole-row sum (pixels below whole_px), or its `parts` part sums added in
+// part order (the tail rows); the slots in queue order (Frame) -- *
+// pixel_sample_scale, to linear f32 (camera.rs:193), and -- when srgb is
+// given -- the pixel's to_rgb bytes from the f64 sum, as the reference
+// converts its f64 color.
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
-                                                       uint32_t parts, double scale, float* __restrict__ out,
-                                                       uint8_t* __restrict__ srgb, int toon) {
+                                                       uint32_t parts, uint32_t whole_px, double scale,
+                                                       float* __restrict__ out, uint8_t* __restrict__ srgb, int toon) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npix) return;
-    const double* src = partial + (uint64_t)p * 3;
-    const uint64_t step = (uint64_t)npix * 3;
+    const bool whole = p < whole_px;
+    const uint32_t np = whole ? 1u : parts;
+    const uint64_t first = whole ? (uint64_t)p * S : (uint64_t)whole_px * S + (uint64_t)(p - whole_px) * S * parts;
+    const double* src = partial + first * 3;
     double r = 0.0, g = 0.0, b = 0.0;
     for (uint32_t k = 0; k < S; ++k) {
-        const double* row = src + (uint64_t)k * parts * step;
+        const double* row = src + (uint64_t)k * np * 3;
         double rr = row[0], rg = row[1], rb = row[2];
-        for (uint32_t j = 1; j < parts; ++j) {
-            rr += row[j * step + 0];
-            rg += row[j * step + 1];
-            rb += row[j * step + 2];
+        for (uint32_t j = 1; j < np; ++j) {
+            rr += row[j * 3 + 0];
+            rg += row[j * 3 + 1];
+            rb += row[j * 3 + 2];
         }
         r += rr;
         g += rg;
@@ -2625,11 +2639,15 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.total_items = fd->W * fd->rows * fd->S;
     F.parts = fd->parts > 1 ? fd->parts : 1u;  // the host's rtk_row_parts: no part empty
     F.part_len = (fd->S + F.parts - 1) / F.parts;
-    F.queue_total = F.total_items * F.parts;
+    const uint32_t whole_rows = fd->whole_rows < fd->rows ? fd->whole_rows : fd->rows;
+    F.whole_items = F.parts > 1 ? fd->W * whole_rows * fd->S : F.total_items;
+    F.queue_total = F.whole_items + (F.total_items - F.whole_items) * F.parts;
     F.static_entries = (uint32_t)grid * (uint32_t)rtk_block_threads(tier);
     F.chunk_min = fd->chunk_min;
     auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
     F.inv_parts = inv_up(F.parts);
+    F.parts_m1 = (float)(F.parts - 1);
+    F.inv_parts_f = 1.0f / (float)F.parts;
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
     F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
@@ -2661,7 +2679,7 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
     const uint32_t npix = fd->W * fd->rows;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((npix + 255) / 256), dim3(256), 0, stream, partial, npix, fd->S,
-                       F.parts, fd->pixel_sample_scale, out, srgb, toon);
+                       F.parts, F.whole_items / fd->S, fd->pixel_sample_scale, out, srgb, toon);
     return hipGetLastError();
 }
 
@@ -2697,15 +2715,28 @@ extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_
     return hipGetLastError();
 }
 
-extern "C" uint32_t rtk_row_parts(uint32_t W, uint32_t H, uint32_t S, uint32_t part_samples, uint64_t budget_bytes) {
+extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples) {
     if (part_samples == 0 || S <= part_samples) return 1;
-    uint32_t parts = (S + part_samples - 1) / part_samples;
-    // within the part-sum budget, and the queue of the whole frame below 2^32 entries
-    while (parts > 1 && ((uint64_t)W * H * S * parts * 3 * sizeof(double) > budget_bytes ||
-                         (uint64_t)W * H * S * parts >= 0xFFF00000ull))
-        --parts;
+    const uint32_t parts = (S + part_samples - 1) / part_samples;
     const uint32_t len = (S + parts - 1) / parts;
     return (S + len - 1) / len;  // as many parts of that length as S takes: none empty
+}
+
+extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint64_t budget_bytes,
+                                  uint32_t permille) {
+    if (parts <= 1 || W == 0 || S == 0) return 0;
+    uint64_t t = ((uint64_t)H * permille + 999) / 1000;
+    if (t > H) t = H;
+    // the tail's part sums beyond one sum per row within the budget
+    const uint64_t extra_row = (uint64_t)W * S * (parts - 1);
+    const uint64_t by_budget = budget_bytes / (extra_row * 3 * sizeof(double));
+    if (t > by_budget) t = by_budget;
+    // the queue of the whole frame below 2^32 entries
+    const uint64_t whole = (uint64_t)W * H * S;
+    if (whole >= 0xFFF00000ull) return 0;
+    const uint64_t by_queue = (0xFFF00000ull - 1 - whole) / extra_row;
+    if (t > by_queue) t = by_queue;
+    return (uint32_t)t;
 }
 
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }

@@ -124,7 +124,7 @@ struct DeviceWorld {
     // the last render on this slot
     bool ran = false;  // the path kernel ran (ev_start / ev_stop are valid)
     uint64_t samples = 0;
-    uint32_t W = 0, rows = 0, S = 0, parts = 1;
+    uint32_t W = 0, rows = 0, S = 0, parts = 1, whole_rows = 0;
     hipStream_t last_stream = nullptr;
 };
 
@@ -563,27 +563,41 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     rtk_frame_desc f;
     if ((rc = init_frame(cam, seed, p.row_offset, p.row_stride, f)) != RT_OK) return fail(rc);
     p.rows = f.rows;
-    // Every stratum row goes out in parts of about RT_PART_SAMPLES (4) samples
-    // (rtk_row_parts; decided on the whole frame, so shards and device counts
-    // sum rows alike): a launch ends on its longest queue entries.
-    // The part-sum buffer is held per scene and device slot (grow-only, freed
-    // with the scene): at most RT_PART_BUDGET_MB (8 GiB) and at most 1/16 of
-    // the device's memory (18 GiB of an MI355X's 288).  A device that cannot
-    // allocate it renders whole rows instead (parts = 1): the same samples,
-    // each row's f64 sum then in one run instead of part sums added in order
-    // (~1 ulp).
-    uint64_t budget = (uint64_t)env_u32("RT_PART_BUDGET_MB", 8192) << 20;
+    // The stratum rows of the frame's last RT_TAIL_PERMILLE / 1000 image rows
+    // (half) go out in parts of about RT_PART_SAMPLES (4) samples, every other
+    // row as one queue entry (rtk_row_parts, rtk_tail_rows; decided on the
+    // whole frame, so shards and device counts sum rows alike): a launch ends
+    // on short queue entries, since each shard's tail rows are its last.
+    // One f64 sum per queue entry: the part-sum buffer (held per scene and
+    // device slot, grow-only, freed with the scene) is one sum per stratum
+    // row plus the tail's extra parts, those within RT_PART_BUDGET_MB (4 GiB)
+    // and 1/64 of the device's memory.  A device that cannot allocate it
+    // renders whole rows only (parts = 1): the same samples, the tail rows'
+    // f64 sums then in one run instead of part sums added in order (~1 ulp).
+    // (DESIGN.md §4 "Tail rows": C2 at a tail of 1/4, 1/2 and the whole frame.)
+    const uint32_t H = rt_camera_image_height(cam);
+    uint64_t budget = (uint64_t)env_u32("RT_PART_BUDGET_MB", 4096) << 20;
     size_t mem_free = 0, mem_total = 0;
-    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && mem_total) budget = std::min<uint64_t>(budget, mem_total / 16);
-    f.parts = rtk_row_parts(f.W, rt_camera_image_height(cam), f.S, env_u32("RT_PART_SAMPLES", 4), budget);
+    if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && mem_total) budget = std::min<uint64_t>(budget, mem_total / 64);
+    f.parts = rtk_row_parts(f.S, env_u32("RT_PART_SAMPLES", 4));
+    const uint32_t tail = rtk_tail_rows(f.W, H, f.S, f.parts, budget, env_u32("RT_TAIL_PERMILLE", 500));
+    if (tail == 0) f.parts = 1;
+    // the shard's rows above the tail: image rows row_offset + r * row_stride < H - tail
+    const uint32_t whole_img = H - tail;
+    f.whole_rows = whole_img > f.row_offset
+                       ? std::min<uint32_t>(f.rows, (whole_img - f.row_offset + f.row_stride - 1) / f.row_stride)
+                       : 0u;
     f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
-    rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * f.parts * 3 * sizeof(double),
-              "hipMalloc partial sums");
+    auto part_sums = [&f]() {
+        return ((size_t)f.W * f.whole_rows * f.S + (size_t)f.W * (f.rows - f.whole_rows) * f.S * f.parts) * 3 *
+               sizeof(double);
+    };
+    rc = grow((void**)&d->partial, d->partial_bytes, part_sums(), "hipMalloc partial sums");
     if (rc != RT_OK && f.parts > 1) {
         (void)hipGetLastError();
         f.parts = 1;
-        rc = grow((void**)&d->partial, d->partial_bytes, (size_t)f.W * f.rows * f.S * 3 * sizeof(double),
-                  "hipMalloc partial sums (whole rows)");
+        f.whole_rows = f.rows;
+        rc = grow((void**)&d->partial, d->partial_bytes, part_sums(), "hipMalloc partial sums (whole rows)");
     }
     if (rc != RT_OK) return fail(rc);
     if (!p.out &&
@@ -627,6 +641,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     d->rows = f.rows;
     d->S = f.S;
     d->parts = f.parts;
+    d->whole_rows = f.parts > 1 ? f.whole_rows : f.rows;
     d->last_stream = p.stream;
 }
 
@@ -968,25 +983,31 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
     (void)hipSetDevice(d->device);
     hipError_t e = hipStreamSynchronize(d->last_stream);
     if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
-    // device slots: (s_i * parts + part) * pixels + pixel (rtk::Frame); a
-    // row's sum = its part sums added in part order, as rt_reduce_kernel adds
+    // device slots in queue order (rtk::Frame): one per stratum row of the
+    // whole rows, `parts` per stratum row of the tail rows; a tail row's sum =
+    // its part sums added in part order, as rt_reduce_kernel adds them
+    const uint64_t npix = (uint64_t)d->W * d->rows, whole_px = (uint64_t)d->W * d->whole_rows;
+    const uint64_t slots = whole_px * d->S + (npix - whole_px) * d->S * d->parts;
     std::vector<double> buf;
     try {
-        buf.resize(n * d->parts);
+        buf.resize(slots * 3);
     } catch (const std::bad_alloc&) {
         return set_error(RT_ENOMEM, "out of host memory");
     }
     if (n && (e = hipMemcpy(buf.data(), d->partial, buf.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "hipMemcpy partials");
-    const uint64_t npix = (uint64_t)d->W * d->rows;
-    for (uint64_t pix = 0; pix < npix; ++pix)
+    for (uint64_t pix = 0; pix < npix; ++pix) {
+        const bool whole = pix < whole_px;
+        const uint32_t np = whole ? 1u : d->parts;
+        const double* px = buf.data() + (whole ? pix * d->S : whole_px * d->S + (pix - whole_px) * d->S * np) * 3;
         for (uint32_t si = 0; si < d->S; ++si)
             for (int c = 0; c < 3; ++c) {
-                const double* src = buf.data() + ((uint64_t)si * d->parts * npix + pix) * 3 + c;
+                const double* src = px + (uint64_t)si * np * 3 + c;
                 double sum = src[0];
-                for (uint32_t j = 1; j < d->parts; ++j) sum += src[j * npix * 3];
+                for (uint32_t j = 1; j < np; ++j) sum += src[j * 3];
                 out[(pix * d->S + si) * 3 + c] = sum;
             }
+    }
     return RT_OK;
 }
 

@@ -25,7 +25,7 @@ import bench  # noqa: E402  (the workloads)
 
 def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
-    spp = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl][1]
+    spp = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "-" else bench.WORKLOADS[wl][1]
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     lib = os.environ.get("RT_LIB")
     api = pkg.load() if not lib else importlib.import_module("raytracer-2025_amd.capi").Api(

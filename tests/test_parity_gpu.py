@@ -190,16 +190,19 @@ def test_shard_rows_equal_full_frame(gpu, rt, scenes):
 
 @pytest.mark.parametrize("spp", [64, 484])
 def test_queue_split_is_partition_independent(gpu, rt, scenes, monkeypatch, spp):
-    """The work queue's split never depends on the partition: stratum rows go
-    out in parts of about RT_PART_SAMPLES samples decided on the whole frame
-    (rtk_row_parts), so every row shard -- one rank of an N-GPU run -- sums
-    its rows as the whole frame does: bit-equal images; and the (pixel, s_i)
-    sums of the partials hook hold every sample whatever the part size."""
+    """The work queue's split never depends on the partition: the stratum rows
+    of the frame's last RT_TAIL_PERMILLE / 1000 image rows go out in parts of
+    about RT_PART_SAMPLES samples, the others whole, decided on the whole
+    frame (rtk_row_parts, rtk_tail_rows), so every row shard -- one rank of an
+    N-GPU run -- sums its rows as the whole frame does: bit-equal images; and
+    the (pixel, s_i) sums of the partials hook hold every sample whatever the
+    part size and the tail's share."""
     scene = rt.Scene(gpu)
     world, lights, cam = scenes.random_spheres(scene, 96, spp)
     runs = []
-    for ps in ("4", "1", "0"):
+    for ps, pm in (("4", "250"), ("1", "250"), ("0", "250"), ("4", "1000"), ("4", "0"), ("2", "500")):
         monkeypatch.setenv("RT_PART_SAMPLES", ps)
+        monkeypatch.setenv("RT_TAIL_PERMILLE", pm)
         lin, _, st = cam.render(world, lights, seed=5, want_srgb=False)
         runs.append((lin, gpu_partials(gpu, scene, cam, lin.shape[0])))
         assert st.samples == 96 * 54 * cam.sqrt_spp ** 2
@@ -207,7 +210,8 @@ def test_queue_split_is_partition_independent(gpu, rt, scenes, monkeypatch, spp)
         np.testing.assert_allclose(part, runs[0][1], rtol=1e-12, atol=1e-300)
         np.testing.assert_allclose(lin, runs[0][0], rtol=1e-6, atol=0)
     monkeypatch.setenv("RT_PART_SAMPLES", "4")
-    for off, stride in ((1, 3), (0, 8)):
+    monkeypatch.setenv("RT_TAIL_PERMILLE", "250")
+    for off, stride in ((1, 3), (0, 8), (5, 8), (7, 8)):
         shard, _, _ = cam.render(world, lights, seed=5, row_offset=off, row_stride=stride, want_srgb=False)
         np.testing.assert_array_equal(shard, runs[0][0][off::stride])
 

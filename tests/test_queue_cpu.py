@@ -1,10 +1,12 @@
-"""The work queue's row parts on CPU (rtk_row_parts in librt_mi355x.so, no
-device needed): every stratum row of sqrt_spp = S samples goes out as `parts`
-queue entries of ceil(S / parts) consecutive samples, summed in part order by
-the reduce (and by rt_render_partials_get).  The split is a function of the
-whole frame -- never of a row shard -- so 1..8 GPUs sum every row alike and
-produce the same bits; no part may be empty (a lane would trace sample S);
-the part sums of the whole frame stay within the memory budget."""
+"""The work queue's split on CPU (rtk_row_parts / rtk_tail_rows in
+librt_mi355x.so, no device needed).  The stratum rows of a frame's last
+image rows -- its tail -- go out as `parts` queue entries of ceil(S / parts)
+consecutive samples each, summed in part order by the reduce (and by
+rt_render_partials_get); every other stratum row is one entry.  The split is a
+function of the whole frame -- never of a row shard -- so 1..8 GPUs sum every
+row alike and produce the same bits; no part may be empty (a lane would trace
+sample S); the tail's extra part sums stay within the memory budget and the
+frame's queue within 2^32 entries."""
 import ctypes
 
 import pytest
@@ -13,19 +15,20 @@ GiB = 1 << 30
 
 
 @pytest.fixture(scope="module")
-def row_parts(product):
+def lib(product):
     import importlib
     lib = ctypes.CDLL(importlib.import_module("raytracer-2025_amd").LIB_PATH)
-    f = lib.rtk_row_parts
-    f.restype = ctypes.c_uint32
-    f.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
-    return f
+    lib.rtk_row_parts.restype = ctypes.c_uint32
+    lib.rtk_row_parts.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+    lib.rtk_tail_rows.restype = ctypes.c_uint32
+    lib.rtk_tail_rows.argtypes = [ctypes.c_uint32] * 4 + [ctypes.c_uint64, ctypes.c_uint32]
+    return lib
 
 
 @pytest.mark.parametrize("S", list(range(1, 70)) + [100, 128, 256, 1000])
-@pytest.mark.parametrize("part_samples", [0, 1, 2, 5, 6, 7, 11, 16])
-def test_parts_cover_the_row_without_empty_parts(row_parts, S, part_samples):
-    p = row_parts(16, 16, S, part_samples, 1 << 62)  # no budget or queue-size cap here
+@pytest.mark.parametrize("part_samples", [0, 1, 2, 4, 5, 6, 7, 11, 16])
+def test_parts_cover_the_row_without_empty_parts(lib, S, part_samples):
+    p = lib.rtk_row_parts(S, part_samples)
     assert p >= 1
     if part_samples == 0 or S <= part_samples:
         assert p == 1
@@ -36,18 +39,43 @@ def test_parts_cover_the_row_without_empty_parts(row_parts, S, part_samples):
     assert p <= S
 
 
-def test_budget_bounds_the_part_sums(row_parts):
-    # C5: 3840 x 2160 at 64^2: whole rows are 12.7 GB of part sums already
-    assert row_parts(3840, 2160, 64, 6, 8 * GiB) == 1
-    # C2 (the headline): 22 samples per row -> 4 parts of 6, 4.4 GB
-    assert row_parts(1920, 1080, 22, 6, 8 * GiB) == 4
-    for W, H, S in ((1920, 1080, 22), (800, 800, 32), (3840, 2160, 16), (1920, 1080, 45)):
-        p = row_parts(W, H, S, 6, 8 * GiB)
-        assert p == 1 or W * H * S * p * 24 <= 8 * GiB
+def test_tail_is_the_asked_share_of_the_frame(lib):
+    # C2 (the headline): 22 samples per stratum row -> 6 parts; the last 1/4
+    # of 1080 rows, 1.4 GB of extra part sums
+    assert lib.rtk_row_parts(22, 4) == 6
+    assert lib.rtk_tail_rows(1920, 1080, 22, 6, 2 * GiB, 250) == 270
+    assert lib.rtk_tail_rows(1920, 1080, 22, 6, 2 * GiB, 125) == 135
+    # the whole frame asked: as many rows as 2 GiB of extra part sums hold
+    assert lib.rtk_tail_rows(1920, 1080, 22, 6, 2 * GiB, 1000) == 2 * GiB // (1920 * 22 * 5 * 24)
+    assert lib.rtk_tail_rows(1920, 1080, 22, 6, 1 << 62, 1000) == 1080
+    # rounds up: a tiny frame still ends on parts
+    assert lib.rtk_tail_rows(16, 9, 4, 2, 1 << 62, 250) == 3
+    # nothing to split
+    assert lib.rtk_tail_rows(1920, 1080, 22, 1, 2 * GiB, 250) == 0
+    assert lib.rtk_tail_rows(1920, 1080, 22, 6, 2 * GiB, 0) == 0
 
 
-def test_queue_of_the_whole_frame_fits_32_bits(row_parts):
-    # 3840 x 2160 at 1000^2 samples: 8.3e12 whole rows already -- no parts
-    assert row_parts(3840, 2160, 1000, 6, 1 << 62) == 1
-    p = row_parts(1920, 1080, 100, 6, 1 << 62)
-    assert p > 1 and 1920 * 1080 * 100 * p < 0xFFF00000
+@pytest.mark.parametrize("W,H,S,ps", [(1920, 1080, 22, 4), (800, 800, 32, 4), (1920, 1080, 16, 4),
+                                      (3840, 2160, 64, 4), (3840, 2160, 16, 4), (1920, 1080, 45, 6)])
+def test_budget_bounds_the_tail_part_sums(lib, W, H, S, ps):
+    p = lib.rtk_row_parts(S, ps)
+    for budget in (GiB // 4, 2 * GiB, 8 * GiB):
+        t = lib.rtk_tail_rows(W, H, S, p, budget, 250)
+        assert t <= -(-H * 250 // 1000)
+        assert t * W * S * (p - 1) * 24 <= budget
+        # as many rows as the budget holds
+        assert t == -(-H * 250 // 1000) or (t + 1) * W * S * (p - 1) * 24 > budget
+    # C5 (3840 x 2160 at 64^2): whole rows are 12.7 GB; the default 2-GiB budget
+    # still gives its launch a tail of parts
+    if (W, H, S) == (3840, 2160, 64):
+        assert lib.rtk_tail_rows(W, H, S, p, 2 * GiB, 250) >= 20
+
+
+def test_queue_of_the_whole_frame_fits_32_bits(lib):
+    # 3840 x 2160 at 1000^2 samples: 8.3e12 whole rows already -- no tail
+    assert lib.rtk_tail_rows(3840, 2160, 1000, 250, 1 << 62, 1000) == 0
+    W, H, S = 1920, 1080, 100
+    p = lib.rtk_row_parts(S, 4)
+    t = lib.rtk_tail_rows(W, H, S, p, 1 << 62, 1000)
+    assert 0 < t < H
+    assert W * H * S + t * W * S * (p - 1) < 0xFFF00000
