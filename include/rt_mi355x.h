@@ -67,11 +67,13 @@ int32_t rt_tex_checker(rt_scene* s, double scale, int32_t even_tex, int32_t odd_
 int32_t rt_tex_image(rt_scene* s, uint32_t width, uint32_t height, const float* rgba, int32_t linear_interp);
 /* ImageTexture::new / new_raw_image (texture.rs:82-97) with the file path
  * given directly (the reference joins RTW_IMAGES or ./assets, image.rs:21-46):
- * the library decodes PNG (rt_png.hpp: the image crate's into_rgba32f, then
- * the sRGB EOTF unless raw, image.rs:63-82).  A file that is missing or fails
- * to decode is the reference's Image::EMPTY (cyan); another format, or an
- * interlaced PNG, is RT_EUNSUPPORTED.  raw != 0: no sRGB conversion
- * (new_raw_image); linear_interp selects ImageInterpMethod::Linear. */
+ * the format comes from the extension as ImageReader::open takes it; the
+ * library decodes PNG, JPEG and Radiance HDR (rt_image.hpp: the image crate's
+ * into_rgba32f, then the sRGB EOTF unless raw or HDR, image.rs:63-82).  A file
+ * that is missing, has no image extension or fails to decode is the
+ * reference's Image::EMPTY (cyan); another image format (GIF, EXR, ...) or a
+ * CMYK / arithmetic-coded / 12-bit JPEG is RT_EUNSUPPORTED.  raw != 0: no sRGB
+ * conversion (new_raw_image); linear_interp selects ImageInterpMethod::Linear. */
 int32_t rt_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t linear_interp);
 /* NoiseTexture::new (texture.rs:183-188).  Perlin tables are drawn from
  * SplitMix64(seed) in the order of perlin.rs:16-36. */

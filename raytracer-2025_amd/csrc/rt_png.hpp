@@ -5,9 +5,9 @@
 // one v / 65535; gray expands to (g, g, g), palette to its RGB, a missing
 // alpha is 1, tRNS keys become alpha 0) and then, unless the texture is raw or
 // the format is HDR / EXR / AVIF, converts RGB with palette's sRGB EOTF
-// (utils/image.rs:21-82).  This restates that pipeline for PNG -- the only
-// image format among the reference's assets besides one JPEG -- over zlib's
-// inflate, interlaced (Adam7) or not.
+// (utils/image.rs:21-82).  This restates that pipeline's PNG decode over
+// zlib's inflate, interlaced (Adam7) or not; rt_image.hpp picks the decoder
+// by extension and applies the EOTF.
 // tests/test_png_cpu.py pins the decoder against PIL on the reference's own
 // PNG assets (8-bit RGB / RGBA / gray, 4-bit palette) and on synthetic files
 // covering every color type, bit depth and filter.
@@ -188,37 +188,6 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
             }
         }
     }
-    return OK;
-}
-
-// Image::new(path, raw) + pixel_data's colour handling (utils/image.rs:21-82)
-// for a path given directly: MISSING (the reference's Image::EMPTY) when the
-// file cannot be opened or decoded as an image; the pixels as linear RGBA f32
-// otherwise (sRGB EOTF on RGB unless raw).
-inline Status load(const std::string& path, bool raw, uint32_t& W, uint32_t& H, std::vector<float>& rgba,
-                   std::string& err) {
-    W = H = 0;
-    rgba.clear();
-    std::FILE* fp = std::fopen(path.c_str(), "rb");
-    if (!fp) return MISSING;
-    std::vector<uint8_t> f;
-    uint8_t buf[65536];
-    size_t n;
-    while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) f.insert(f.end(), buf, buf + n);
-    std::fclose(fp);
-    Status st = decode(f, W, H, rgba, err);
-    if (st == CORRUPT) {  // ImageReader::decode().ok()? -> None -> Image::EMPTY
-        W = H = 0;
-        rgba.clear();
-        return MISSING;
-    }
-    if (st != OK) {
-        err = path + ": " + err;
-        return st;
-    }
-    if (!raw)
-        for (size_t i = 0; i < rgba.size(); i += 4)
-            for (int c = 0; c < 3; ++c) rgba[i + c] = srgb_to_linear(rgba[i + c]);
     return OK;
 }
 

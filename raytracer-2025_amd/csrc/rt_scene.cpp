@@ -1,7 +1,7 @@
 // rt_scene.cpp -- builder half of the C ABI (include/rt_mi355x.h) and the
 // world flattener.  Host code only; the device half is rt_render.hip.
 #include "rt_kernel.h"
-#include "rt_png.hpp"
+#include "rt_image.hpp"
 #include "rt_qnode.h"
 #include "rt_scene.hpp"
 
@@ -942,8 +942,8 @@ int32_t rt_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t li
     uint32_t w = 0, h = 0;
     std::vector<float> px;
     std::string err;
-    const rtpng::Status st = rtpng::load(path, raw != 0, w, h, px, err);
-    if (st == rtpng::UNSUPPORTED) return set_error(RT_EUNSUPPORTED, err);
+    const rtimg::Status st = rtimg::load(path, raw != 0, w, h, px, err);
+    if (st == rtimg::UNSUPPORTED) return set_error(RT_EUNSUPPORTED, err);
     return rt_tex_image(s, w, h, px.empty() ? nullptr : px.data(), linear);  // MISSING: 0 x 0, cyan
 }
 int32_t rt_tex_noise(rt_scene* s, double scale, uint64_t seed) {

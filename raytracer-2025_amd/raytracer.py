@@ -109,7 +109,8 @@ class Scene:
 
     def ImageTexture_file(self, path, raw=False, linear_interp=None):
         """ImageTexture::new(file) / new_raw_image(file) (texture.rs:82-97) with
-        the path given directly; PNG decoded by the library (missing -> cyan)."""
+        the path given directly; PNG, JPEG and Radiance HDR decoded by the
+        library, the format taken from the extension (missing -> cyan)."""
         interp = raw if linear_interp is None else linear_interp
         return Texture(self, self._c(self.api.tex_image_file(self.s, os.fsencode(path), int(raw), int(interp))))
 

@@ -1,5 +1,5 @@
-// TEST HARNESS: decodes one file with raytracer-2025_amd/csrc/rt_png.hpp (the
-// library's ImageTexture loader) or, built with -DORACLE_PNG, with the
+// TEST HARNESS: decodes one file with raytracer-2025_amd/csrc/rt_image.hpp (the
+// library's ImageTexture loader: rt_png.hpp for a .png) or, built with -DORACLE_PNG, with the
 // oracle's own reader (oracle/orc_png.hpp), and writes "status width height"
 // and then width*height*4 f32 values (row-major RGBA) to the output file, for
 // tests/test_png_cpu.py to compare with PIL.  Status: 0 decoded, 1 no image
@@ -12,7 +12,7 @@
 #ifdef ORACLE_PNG
 #include "../../oracle/orc_png.hpp"
 #else
-#include "../../raytracer-2025_amd/csrc/rt_png.hpp"
+#include "../../raytracer-2025_amd/csrc/rt_image.hpp"
 #endif
 
 int main(int argc, char** argv) {
@@ -28,7 +28,7 @@ int main(int argc, char** argv) {
             for (int c = 0; c < 3; ++c) px[i + c] = orcpng::eotf(px[i + c]);
     if (st != orcpng::DECODED) w = h = 0, px.clear();
 #else
-    int st = (int)rtpng::load(argv[1], raw, w, h, px, err);
+    int st = (int)rtimg::load(argv[1], raw, w, h, px, err);
 #endif
     std::FILE* f = std::fopen(argv[2], "wb");
     if (!f) return 3;

@@ -233,6 +233,53 @@ def test_image_texture(gpu, oracle, rt, linear):
     assert st["gpu"].panics == 0
 
 
+@pytest.mark.parametrize("fmt", ["jpeg420", "jpeg_progressive", "hdr"])
+def test_image_texture_file_formats(gpu, oracle, rt, tmp_path, fmt):
+    """ImageTexture::new_raw_image(file) (texture.rs:82-97) from a JPEG (4:2:0
+    baseline / progressive, rt_jpeg.hpp) or a Radiance HDR (rt_hdr.hpp, linear
+    whatever the raw flag: image.rs:76-80) decoded by the library, against the
+    oracle given the same pixels decoded independently -- PIL for the JPEG
+    (tests/test_jpeg_cpu.py holds the decoder bit-exact against it), the
+    RGBE formula for the HDR."""
+    PILImage = pytest.importorskip("PIL.Image")
+    rng = np.random.default_rng(11)
+    h, w = 40, 56
+    if fmt.startswith("jpeg"):
+        a = (_image(h, w, 4)[..., :3] * 255).astype(np.uint8)
+        path = tmp_path / "t.jpg"
+        PILImage.fromarray(a).save(str(path), quality=85, subsampling=2, progressive=fmt == "jpeg_progressive")
+        px = np.asarray(PILImage.open(str(path)).convert("RGB"), dtype=np.float32) / np.float32(255.0)
+    else:
+        from test_jpeg_cpu import _hdr_bytes, _rgbe_expected
+        rgbe = rng.integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+        rgbe[..., 3] = rng.integers(125, 131, size=(h, w))
+        path = tmp_path / "t.hdr"
+        path.write_bytes(_hdr_bytes(rgbe, "new_rle"))
+        px = _rgbe_expected(rgbe)
+    rgba = np.concatenate([px, np.ones((h, w, 1), np.float32)], axis=-1)
+
+    def build(s):
+        if s.api is gpu:
+            tex = s.ImageTexture_file(str(path), raw=True, linear_interp=True)
+        else:
+            tex = s.ImageTexture(rgba, linear_interp=True)
+        world = s.Hittables()
+        world.add(s.Sphere((0, 1, 0), 1.0, s.Lambertian(tex)))
+        world.add(s.Quad((-3, 0, -3), (6, 0, 0), (0, 0, 6), s.Lambertian(tex)))
+        cam = rt.Camera()
+        cam.aspect_ratio = 16 / 9
+        cam.image_width = 96
+        cam.samples_per_pixel = 16
+        cam.max_depth = 8
+        cam.vertical_fov_in_degrees = 35.0
+        cam.look_from = (5.0, 2.0, 6.0)
+        cam.look_at = (0.0, 0.7, 0.0)
+        return world, None, cam
+    out, st = render_both(gpu, oracle, rt, build)
+    check(out)
+    assert st["gpu"].panics == 0
+
+
 @pytest.mark.parametrize("names", [["tile", "glass", "bumpy"], ["lamp", "leaf", "lampleaf"]])
 def test_obj_image_materials(gpu, oracle, rt, capi, tmp_path, names):
     """map_Kd -> ImageTexture (a vanilla Metal takes its pixel at (0, 0), a
