@@ -586,6 +586,9 @@ __device__ __forceinline__ double f4_hi(float4 q) { return __hiloint2double(__fl
 #endif
 template <int TIER>
 constexpr bool flat_runs() { return TIER == TIER_FULL_FLAT && RT_FLAT_RUNS; }
+#ifndef RT_FLAT_MEDIA_IN_LIST
+#define RT_FLAT_MEDIA_IN_LIST 1  // the flat tier queues a list's media in the list step
+#endif
 #ifndef RT_FLAT_BOUNDARY_BOXES
 #define RT_FLAT_BOUNDARY_BOXES 0  // the medium boundary walks test element boxes too
 #endif
@@ -1006,10 +1009,20 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
         const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
         if constexpr (flat_boxes<TIER>()) {
             const uint32_t ck = ref_kind(child);
-            if (ck != K_SPHERE && ck != K_QUAD && ck != K_TRI && ck != K_MSPHERE &&
-                !list_box_hit(S, li, make_rayf(r), tmin_f, T.cl.c_f)) {
-                T.cur = nxt;
-                return true;
+            if (ck != K_SPHERE && ck != K_QUAD && ck != K_TRI && ck != K_MSPHERE) {
+                const bool in_box = list_box_hit(S, li, make_rayf(r), tmin_f, T.cl.c_f);
+                // a ConstantMedium element whose box the ray meets is queued
+                // for the media phase right here (K_MEDIUM below), without a
+                // step of its own and the pop of the rest of the list
+                const bool queue = RT_FLAT_MEDIA_IN_LIST && in_box && ck == K_MEDIUM && T.nmed < RT_MEDIA_CAP;
+                if (queue) {
+                    med[T.nmed * RT_BLOCK] = make_uint4(ref_index(child), T.nxf, T.xfs.a, T.xfs.b);
+                    ++T.nmed;
+                }
+                if (!in_box || queue) {
+                    T.cur = nxt;
+                    return true;
+                }
             }
         }
         const uint32_t ck = ref_kind(child);
