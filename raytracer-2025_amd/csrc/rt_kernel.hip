@@ -993,7 +993,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
             const uint32_t ck0 = ref_kind(child);
             if (ck0 == K_QUAD || ck0 == K_TRI) {
                 const uint32_t run = S.list_boxes[li].run, n = run & 0xffu, first = ref_index(child);
-                RT_DIAG_ONLY(++dg.lane_trace_iters; dg.sphere_tests += n;)
+                RT_DIAG_ONLY(dg.sphere_tests += n;)
                 for (uint32_t k = 0; k < n; ++k) {
                     const bool tri = (run >> (8u + k)) & 1u;
                     double tt;
@@ -1039,7 +1039,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
     const uint32_t this_ref = cur;
     double t;
     bool got = false;
-    RT_DIAG_ONLY(++dg.lane_trace_iters; if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
+    RT_DIAG_ONLY(if (kind == K_BVH) ++dg.node_visits; if (kind == K_SPHERE || kind == K_TRI || kind == K_QUAD) ++dg.sphere_tests;)
     if (unified_load<TIER>() && (kind == K_BVH || kind == K_SPHERE || kind == K_TRI || kind == K_QUAD)) {
         // One load for the step's record, whatever it is: a node's 7 rows, a
         // quad's / triangle's 128 B, a sphere's 32 B, read as 8 dwordx4 from
@@ -2296,7 +2296,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if constexpr (TIER == TIER_BASIC && RT_BVH4) {
                 return trace4_step(S, ray, T, stk, pq, (const RT_LDS float4*)node_lds, dg);
             } else {
-                RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
+                // every step call of the lane (the basic tier counts its own)
+                RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters; ++dg.lane_trace_iters;)
                 if constexpr (PARK_RAY)
                     return trace_step<TIER>(S, RayLds{pst + 9 * RT_BLOCK}, T, stk, rng, med, dg);
                 else
