@@ -63,6 +63,7 @@ struct Diag {
     unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
     unsigned long long load_cyc = 0, loads = 0;  // -DRT_DIAG_LOADLAT: node-load latency (first active lane)
     unsigned long long pops = 0, pop_reads = 0;  // basic tier: pops and the stack entries they read
+    unsigned long long big_tests = 0, big_hits = 0;  // basic tier: exact tests of spheres with r > 100 (and hits)
 #endif
 };
 #ifdef RT_DIAG
@@ -1438,7 +1439,9 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     if (round) {  // sphere round (sphere.rs:77-108)
         RT_DIAG_ONLY(++dg.sphere_tests;)
         double t;
+        RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_tests;)
         if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
+            RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_hits;)
             T.cl.lower(t);
             T.found = true;
             T.hit.t = t;
@@ -2397,6 +2400,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     atomicAdd(&g_diag[10], dg.loads);
     atomicAdd(&g_diag[11], dg.pops);
     atomicAdd(&g_diag[12], dg.pop_reads);
+    atomicAdd(&g_diag[14], dg.big_tests);
+    atomicAdd(&g_diag[15], dg.big_hits);
 #endif
 #ifdef RT_WAVE_TRACE
     if (trace_lane < RT_TRACE_LANES) {

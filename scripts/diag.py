@@ -58,6 +58,8 @@ out = {
     "node_load_wave_cycles": c[9] / c[10] if c[10] else None,
     "stack_reads_per_pop": c[12] / c[11] if c[11] else None,
     "pops_per_ray": c[11] / c[8],
-    "raw": c[:14],
+    "big_sphere_exact_tests_per_ray": c[14] / c[8],  # basic tier: spheres with r > 100 (C2's ground)
+    "big_sphere_exact_hits_per_ray": c[15] / c[8],
+    "raw": c[:16],
 }
 print(json.dumps(out, indent=1))
