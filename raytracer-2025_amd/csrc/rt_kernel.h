@@ -91,7 +91,10 @@ struct rtk_frame_desc {
     // (rtk::Frame; rtk_row_parts, rtk_tail_rows), summed in part order
     uint32_t parts;
     uint32_t chunk_min;  // smallest guided chunk of queue entries (0: what the wave needs)
-    uint32_t whole_rows, pad2;
+    uint32_t whole_rows;
+    uint32_t chunk_cap;  // most entries per queue atomic (0: the tier's RT_QUEUE_CHUNK[_MESH])
+    uint32_t guide;      // guided chunks: work left / (waves x guide) (0: RT_QUEUE_GUIDE)
+    uint32_t pad2;
 
     double recip_sqrt_spp, pixel_sample_scale;
     double center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3];

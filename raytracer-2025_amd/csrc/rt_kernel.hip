@@ -105,6 +105,7 @@ struct Frame {
     uint32_t parts, part_len, queue_total, whole_items;
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
+    uint32_t chunk_cap;  // largest guided chunk
     // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
     // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
     double inv_parts, inv_S, inv_W;
@@ -2200,9 +2201,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 // in samples than the tail's pools (it would outlast them)
                 const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
                 const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
-                constexpr uint32_t CAP = TIER == TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK;
                 const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
-                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), CAP);
+                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), F.chunk_cap);
                 chunk = max(max(chunk, F.chunk_min), avail < n ? n - avail : 0u);
             }
 #endif
@@ -2664,7 +2664,8 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.inv_parts_f = 1.0f / (float)F.parts;
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
-    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * RT_QUEUE_GUIDE);
+    F.chunk_cap = fd->chunk_cap ? fd->chunk_cap : (tier == rtk::TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK);
+    F.inv_guide = 1.0f / (float)((uint64_t)grid * (rtk_block_threads(tier) / 64) * (fd->guide ? fd->guide : RT_QUEUE_GUIDE));
     F.defocus = fd->defocus;
     F.recip_sqrt_spp = fd->recip_sqrt_spp;
     F.pixel_sample_scale = fd->pixel_sample_scale;

@@ -588,6 +588,8 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
                        ? std::min<uint32_t>(f.rows, (whole_img - f.row_offset + f.row_stride - 1) / f.row_stride)
                        : 0u;
     f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
+    f.chunk_cap = env_u32("RT_CHUNK_CAP", 0);  // A/B knobs (0: the kernel's defaults)
+    f.guide = env_u32("RT_CHUNK_GUIDE", 0);
     auto part_sums = [&f]() {
         return ((size_t)f.W * f.whole_rows * f.S + (size_t)f.W * (f.rows - f.whole_rows) * f.S * f.parts) * 3 *
                sizeof(double);
