@@ -116,6 +116,13 @@ struct Frame {
     D3 center, pixel00, du, dv, disk_u, disk_v;
 };
 
+#ifndef RT_AB_XLOAD
+#define RT_AB_XLOAD 0
+#endif
+#if RT_AB_XLOAD
+__device__ uint32_t g_ab_sink;
+#endif
+
 // n / d for n < 2^32, d < 2^20, from inv = 1/d rounded up: n * inv is at least
 // the quotient's integer part when d divides n (a representable product,
 // rounded to nearest, cannot fall below it) and below the next integer
@@ -1067,6 +1074,14 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
         float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4, q7 = q4;
         if (planar || (kind == K_BVH && !qn)) q4 = q[4], q5 = q[5], q6 = q[6];
         if (planar) q7 = q[7];
+#if RT_AB_XLOAD
+        {  // A/B experiment only: RT_AB_XLOAD more dwordx4 loads per walk step (the vector-memory path's cost)
+            float xs = 0.0f;
+#pragma unroll
+            for (int i = 0; i < RT_AB_XLOAD; ++i) xs += q[8 + i].x;
+            if (__float_as_uint(xs) == 0x7fc01234u) g_ab_sink = 1u;
+        }
+#endif
         if (kind == K_BVH) {
             if (qn)
                 T.cur = visit4q_rows(q0, q1, q2, q3, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
