@@ -116,6 +116,31 @@ struct Frame {
     D3 center, pixel00, du, dv, disk_u, disk_v;
 };
 
+#ifndef RT_SC_LDS
+// basic tier: the correctly rounded sincos reads its sin / cos (k pi/128)
+// records from an LDS copy of the table (8 KiB) instead of global memory
+#define RT_SC_LDS 0
+#endif
+#if RT_SC_LDS
+__shared__ double g_sc_lds[256 * 4];
+struct ScTabLds {
+    __device__ __forceinline__ void operator()(int k, rtcr::DD& S, rtcr::DD& C) const {
+        const uint32_t i = (uint32_t)(k & 255) * 4u;
+        S = rtcr::DD{g_sc_lds[i], g_sc_lds[i + 1]};
+        C = rtcr::DD{g_sc_lds[i + 2], g_sc_lds[i + 3]};
+    }
+};
+#endif
+template <int TIER>
+__device__ __forceinline__ void t_sincos(double x, double* s, double* c) {
+#if RT_SC_LDS
+    if constexpr (TIER == TIER_BASIC) {
+        k_sincos_tab(x, s, c, ScTabLds{});
+        return;
+    }
+#endif
+    k_sincos(x, s, c);
+}
 #ifndef RT_AB_XLOAD
 #define RT_AB_XLOAD 0
 #endif
@@ -1857,7 +1882,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     if constexpr (HOIST) {
         xi0 = rng.next(ovf);
         xi1 = rng.next(ovf);
-        k_sincos(2.0 * PI * xi0, &sn0, &cs0);
+        t_sincos<TIER>(2.0 * PI * xi0, &sn0, &cs0);
     }
     if constexpr (TIER == TIER_FULL_GL) {
         if (M.flags & MF_EMISSIVE) L = L + beta * emitted_tree<RT_MAT_DEPTH>(S, rec.mat, rec.u, rec.v, rec.p);
@@ -2135,6 +2160,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         const uint32_t n_lds = min(S.n_nodes4, NODE_LDS_CAP);  // == n_nodes4 (launcher)
         const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
         for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) node_lds[k] = src[k];
+#if RT_SC_LDS
+        for (uint32_t k = threadIdx.x; k < 256u * 4u; k += BLK) g_sc_lds[k] = (&RTCR_SC_PIO128[0][0])[k];
+#endif
         __syncthreads();
     }
     if constexpr (tier_full_bvh(TIER) && RT_PERLIN_LDS) {
@@ -2278,7 +2306,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
                 const double rr = sqrt(rng.next(ovf));
                 double sn, cs;
-                k_sincos(theta, &sn, &cs);
+                t_sincos<TIER>(theta, &sn, &cs);
                 origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
             }
             ray.o = origin;
