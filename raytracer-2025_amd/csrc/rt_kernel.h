@@ -94,7 +94,7 @@ struct rtk_frame_desc {
     uint32_t whole_rows;
     uint32_t chunk_cap;  // most entries per queue atomic (0: the tier's RT_QUEUE_CHUNK[_MESH])
     uint32_t guide;      // guided chunks: work left / (waves x guide) (0: RT_QUEUE_GUIDE)
-    uint32_t pad2;
+    uint32_t chunk_min_whole;  // smallest guided chunk while whole-row entries are left
 
     double recip_sqrt_spp, pixel_sample_scale;
     double center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3];

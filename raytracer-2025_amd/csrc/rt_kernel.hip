@@ -106,6 +106,7 @@ struct Frame {
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
     uint32_t chunk_cap;  // largest guided chunk
+    uint32_t chunk_min_whole;  // smallest guided chunk while whole-row entries are left
     // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
     // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
     double inv_parts, inv_S, inv_W;
@@ -2246,7 +2247,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
                 const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
                 chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), F.chunk_cap);
-                chunk = max(max(chunk, F.chunk_min), avail < n ? n - avail : 0u);
+                chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
             }
 #endif
             if (avail < n) {
@@ -2701,6 +2702,7 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     F.queue_total = F.whole_items + (F.total_items - F.whole_items) * F.parts;
     F.static_entries = (uint32_t)grid * (uint32_t)rtk_block_threads(tier);
     F.chunk_min = fd->chunk_min;
+    F.chunk_min_whole = fd->chunk_min_whole;
     auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
     F.inv_parts = inv_up(F.parts);
     F.parts_m1 = (float)(F.parts - 1);

@@ -587,9 +587,12 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     f.whole_rows = whole_img > f.row_offset
                        ? std::min<uint32_t>(f.rows, (whole_img - f.row_offset + f.row_stride - 1) / f.row_stride)
                        : 0u;
-    f.chunk_min = env_u32("RT_CHUNK_MIN", 0);
+    // guided chunks of at least 64 entries, one per lane of the wave (DESIGN §4
+    // "Tail rows": C2 -0.4 % frame, -2.3 % worst 1/8 shard; C3 -0.3 %; C4 +-0)
+    f.chunk_min = env_u32("RT_CHUNK_MIN", 64);
     f.chunk_cap = env_u32("RT_CHUNK_CAP", 0);  // A/B knobs (0: the kernel's defaults)
     f.guide = env_u32("RT_CHUNK_GUIDE", 0);
+    f.chunk_min_whole = env_u32("RT_CHUNK_MIN_WHOLE", 0);
     auto part_sums = [&f]() {
         return ((size_t)f.W * f.whole_rows * f.S + (size_t)f.W * (f.rows - f.whole_rows) * f.S * f.parts) * 3 *
                sizeof(double);
