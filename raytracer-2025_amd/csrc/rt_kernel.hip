@@ -1239,6 +1239,9 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #ifndef RT_SLOT_BALLOT
 #define RT_SLOT_BALLOT 1
 #endif
+#ifndef RT_SORT4
+#define RT_SORT4 1  // basic tier: the hit children sorted by entry distance before the pushes
+#endif
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
 // lane's LDS queue, pq[k * RT_BLOCK_BASIC], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
@@ -1314,6 +1317,7 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
         ref[i] = R[i];
     }
 #endif
+#if RT_SORT4
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];
@@ -1332,6 +1336,23 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
     if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
     if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
     return key[0] < INF ? ref[0] : REF_NONE;
+#else
+    // the nearest hit child is walked next; the others are pushed in slot
+    // order, unsorted (A/B option)
+    float bk = key[0];
+    uint32_t bi = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+        const bool lt = key[i] < bk;
+        bk = lt ? key[i] : bk;
+        bi = lt ? (uint32_t)i : bi;
+    }
+#pragma unroll
+    for (int i = 3; i >= 0; --i)
+        if ((uint32_t)i != bi && key[i] < INF) stk.push(sp++, ref[i], key[i]);
+    const uint32_t br = bi == 0 ? ref[0] : bi == 1 ? ref[1] : bi == 2 ? ref[2] : ref[3];
+    return bk < INF ? br : REF_NONE;
+#endif
 }
 
 // One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
