@@ -188,7 +188,7 @@ def test_shard_rows_equal_full_frame(gpu, rt, scenes):
         np.testing.assert_array_equal(part, full[off::stride])
 
 
-@pytest.mark.parametrize("spp", [64, 484])
+@pytest.mark.parametrize("spp", [64, 484, 4096])
 def test_queue_split_is_partition_independent(gpu, rt, scenes, monkeypatch, spp):
     """The work queue's split never depends on the partition: the stratum rows
     of the frame's last RT_TAIL_PERMILLE / 1000 image rows go out in parts of
