@@ -2302,7 +2302,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
                 const bool whole = q < F.whole_items;
-                const uint32_t qt = q - F.whole_items, it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
+                const uint32_t qt = whole ? 0u : q - F.whole_items;  // (udiv_inv wants n < 2^32 in range)
+                const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
                 const uint32_t item = whole ? q : F.whole_items + it;
                 s_j = whole ? 0u : part * F.part_len;
                 acc = d3(0, 0, 0);
