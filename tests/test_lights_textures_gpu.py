@@ -280,6 +280,51 @@ def test_image_texture_file_formats(gpu, oracle, rt, tmp_path, fmt):
     assert st["gpu"].panics == 0
 
 
+def test_obj_jpeg_maps(gpu, oracle, rt, tmp_path):
+    """An OBJ whose map_Kd / map_Ke / map_Bump images are JPEGs (4:2:0, one
+    progressive): the library decodes them (rt_jpeg.hpp) on the GPU side; the
+    oracle, which reads PNG only, gets the same scene with each JPEG replaced
+    by a PNG of PIL's decode of it (tests/test_jpeg_cpu.py holds the two
+    decodes bit-equal) -- so the JPEG path through the OBJ loader is checked
+    against the oracle at the default bar."""
+    PILImage = pytest.importorskip("PIL.Image")
+    names = ["tile", "glass", "lamp", "bumpy"]
+    dirs = {}
+    for side in ("gpu", "oracle"):
+        d = tmp_path / side
+        d.mkdir()
+        objimg.write_scene(d, names)
+        dirs[side] = d
+    mtl = (dirs["gpu"] / "m.mtl").read_text()
+    for k, img in enumerate(("albedo", "emit", "normal")):
+        src = dirs["gpu"] / f"{img}.png"
+        jpg = dirs["gpu"] / f"{img}.jpg"
+        PILImage.open(str(src)).convert("RGB").save(str(jpg), quality=88, subsampling=2, progressive=k == 1)
+        mtl = mtl.replace(f"{img}.png", f"{img}.jpg")
+        # the oracle's PNG: PIL's decode of that JPEG, lossless
+        PILImage.open(str(jpg)).convert("RGB").save(str(dirs["oracle"] / f"{img}.png"))
+    (dirs["gpu"] / "m.mtl").write_text(mtl)
+
+    def build(s):
+        d = dirs["gpu"] if s.api is gpu else dirs["oracle"]
+        world = s.Hittables()
+        world.add(s.Wavefont(str(d / "scene.obj")))
+        world.add(s.Sphere((0, -100.2, 0), 100, s.Lambertian(s.SolidColor((0.4, 0.45, 0.4)))))
+        cam = rt.Camera()
+        cam.aspect_ratio = 16 / 9
+        cam.image_width = 96
+        cam.samples_per_pixel = 16
+        cam.max_depth = 12
+        cam.vertical_fov_in_degrees = 50.0
+        cam.look_from = (0.0, 1.2, 4.0)
+        cam.look_at = (-0.4, 0.6, 0.0)
+        cam.background = s.SkyGradient((1.0, 1.0, 1.0), (0.5, 0.7, 1.0))
+        return world, None, cam
+    out, st = render_both(gpu, oracle, rt, build)
+    check(out)
+    assert st["gpu"].panics == st["oracle"].panics == 0
+
+
 @pytest.mark.parametrize("names", [["tile", "glass", "bumpy"], ["lamp", "leaf", "lampleaf"]])
 def test_obj_image_materials(gpu, oracle, rt, capi, tmp_path, names):
     """map_Kd -> ImageTexture (a vanilla Metal takes its pixel at (0, 0), a
