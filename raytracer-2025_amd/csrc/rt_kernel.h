@@ -127,6 +127,11 @@ extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples);
 // shard's tail rows are its last rows, so every shard ends on short entries.
 extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint64_t budget_bytes,
                                   uint32_t permille);
+// The rows of a shard (image rows row_offset + r * row_stride, r < rows) above
+// a frame's tail of `tail` rows: its first rtk_shard_whole_rows rows; the rest
+// are tail rows, each shard's last.
+extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row_offset, uint32_t row_stride,
+                                         uint32_t rows);
 // Re-interleaves a gathered frame: staging holds `parts` slices of `slice`
 // floats, slice k = the compact rows k, k + parts, ... of the frame; out gets
 // the frame's `rows` compact rows (rows x W x 3 f32).

@@ -2822,6 +2822,15 @@ extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t p
     return (uint32_t)t;
 }
 
+extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row_offset, uint32_t row_stride,
+                                         uint32_t rows) {
+    const uint32_t whole_img = tail < H ? H - tail : 0u;
+    const uint32_t stride = row_stride ? row_stride : 1u;
+    if (whole_img <= row_offset) return 0u;
+    const uint32_t n = (whole_img - row_offset + stride - 1) / stride;
+    return n < rows ? n : rows;
+}
+
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
 
 

@@ -583,10 +583,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     const uint32_t tail = rtk_tail_rows(f.W, H, f.S, f.parts, budget, env_u32("RT_TAIL_PERMILLE", 500));
     if (tail == 0) f.parts = 1;
     // the shard's rows above the tail: image rows row_offset + r * row_stride < H - tail
-    const uint32_t whole_img = H - tail;
-    f.whole_rows = whole_img > f.row_offset
-                       ? std::min<uint32_t>(f.rows, (whole_img - f.row_offset + f.row_stride - 1) / f.row_stride)
-                       : 0u;
+    f.whole_rows = rtk_shard_whole_rows(H, tail, f.row_offset, f.row_stride, f.rows);
     // guided chunks of at least 64 entries, one per lane of the wave (DESIGN §4
     // "Tail rows": C2 -0.4 % frame, -2.3 % worst 1/8 shard; C3 -0.3 %; C4 +-0)
     f.chunk_min = env_u32("RT_CHUNK_MIN", 64);

@@ -79,3 +79,23 @@ def test_queue_of_the_whole_frame_fits_32_bits(lib):
     t = lib.rtk_tail_rows(W, H, S, p, 1 << 62, 1000)
     assert 0 < t < H
     assert W * H * S + t * W * S * (p - 1) < 0xFFF00000
+
+
+@pytest.mark.parametrize("H,tail", [(1080, 540), (1080, 0), (1080, 1080), (54, 14), (7, 3), (2160, 48)])
+def test_shard_tails_are_each_shards_last_rows(lib, H, tail):
+    """rtk_shard_whole_rows: for every partition of the frame into N row
+    interleaved shards (rows k, k + N, ...), a shard's whole rows are exactly
+    its rows above the frame's tail and come first, so the shards' whole rows
+    together are the frame's H - tail rows and each shard ends on tail rows."""
+    f = lib.rtk_shard_whole_rows
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32] * 5
+    for n in (1, 2, 3, 4, 7, 8):
+        total = 0
+        for k in range(n):
+            rows = len(range(k, H, n))
+            w = f(H, tail, k, n, rows)
+            img = [k + r * n for r in range(rows)]
+            assert all(y < H - tail for y in img[:w]) and all(y >= H - tail for y in img[w:])
+            total += w
+        assert total == H - tail
