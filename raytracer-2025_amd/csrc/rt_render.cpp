@@ -259,6 +259,13 @@ static int prepare_tier(HostWorld& hw) {
             return -1;
         }
     }
+    // mesh / full tiers walk their nodes from global memory: lay them (and
+    // the primitives they name) out for the walk (rth::bvh4_relayout);
+    // RT_BVH4_LAYOUT=<mode> in the environment overrides the default (A/B)
+    if (tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
+        const char* l = std::getenv("RT_BVH4_LAYOUT");
+        bvh4_relayout(hw, l && l[0] ? std::atoi(l) : RT_BVH4_LAYOUT);
+    }
     // mesh / full tiers of a kernel built with RT_QNODES: 64-B quantized nodes
     // (rt_qnode.h) unless a bound is not finite (then the 112-B f32 nodes);
     // RT_QNODES=0 in the environment keeps f32 nodes (A/B)

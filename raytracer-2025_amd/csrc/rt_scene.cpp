@@ -1433,6 +1433,55 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
     return sn;
 }
 
+void bvh4_relayout(HostWorld& hw, int mode) {
+    using rtk::REF_NONE;
+    if (mode <= 0 || hw.nodes4.empty()) return;
+    const size_t n = hw.nodes4.size();
+    // new position of each node: a node's inner children get consecutive
+    // slots (so the siblings a walk pops are neighbours), depth first
+    std::vector<uint32_t> at(n, REF_NONE), order;
+    order.reserve(n);
+    std::vector<uint32_t> todo;
+    auto place = [&](uint32_t ref) {
+        if (rtk::ref_kind(ref) != rtk::K_BVH) return false;
+        const uint32_t i = rtk::ref_index(ref);
+        if (i >= n || at[i] != REF_NONE) return false;
+        at[i] = (uint32_t)order.size();
+        order.push_back(i);
+        return true;
+    };
+    auto lay = [&](uint32_t root) {
+        if (!place(root)) return;
+        todo.push_back(rtk::ref_index(root));
+        while (!todo.empty()) {
+            const uint32_t i = todo.back();
+            todo.pop_back();
+            uint32_t placed[4], np = 0;
+            for (int s = 0; s < 4; ++s)
+                if (place(hw.nodes4[i].ref[s])) placed[np++] = rtk::ref_index(hw.nodes4[i].ref[s]);
+            while (np) todo.push_back(placed[--np]);  // the first child's subtree next
+        }
+    };
+    lay(hw.world_root);
+    for (uint32_t r : hw.list_children) lay(r);
+    for (const rtk::DXform& x : hw.xforms) lay(x.child);
+    for (const rtk::DMedium& m : hw.media) lay(m.boundary);
+    if (order.size() != n) return;  // a node no root reaches: keep the build order
+    auto remap = [&](uint32_t r) {
+        return rtk::ref_kind(r) == rtk::K_BVH ? rtk::make_ref(rtk::K_BVH, at[rtk::ref_index(r)]) : r;
+    };
+    std::vector<rtk::DNode4> nodes(n);
+    for (size_t k = 0; k < n; ++k) {
+        nodes[k] = hw.nodes4[order[k]];
+        for (int s = 0; s < 4; ++s) nodes[k].ref[s] = remap(nodes[k].ref[s]);
+    }
+    hw.nodes4 = std::move(nodes);
+    hw.world_root = remap(hw.world_root);
+    for (uint32_t& r : hw.list_children) r = remap(r);
+    for (rtk::DXform& x : hw.xforms) x.child = remap(x.child);
+    for (rtk::DMedium& m : hw.media) m.boundary = remap(m.boundary);
+}
+
 bool bvh4_quantize(HostWorld& hw) {
     std::vector<rtk::DNode4Q> q(hw.nodes4.size());
     for (size_t k = 0; k < hw.nodes4.size(); ++k) {
