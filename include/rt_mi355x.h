@@ -261,6 +261,20 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values);
  * ln / acos / atan2 = glibc's); impl 1: ROCm's device libm (ocml).  Blocking. */
 int32_t rt_math_selftest(int32_t fn, int32_t impl, const double* a, const double* b, double* out, uint64_t n);
 
+/* Test hook (host only, not part of the reference surface): builds
+ * BVH::from_vec (bvh.rs:16-46) over the children of `list` twice, on copies
+ * of the scene -- the parallel builder rt_bvh_new uses and the plain serial
+ * recursion -- and returns 1 when the two give the same nodes (ids, children,
+ * boxes bit for bit), 0 when they differ, < 0 on a bad argument.  The scene
+ * is not modified. */
+int32_t rt_bvh_selftest(rt_scene* s, int32_t list);
+/* Test hook (host only): flattens (world, lights, background) for rt_render
+ * twice -- the binned-SAH rebuild with both halves of large nodes built at
+ * once, and serially -- and returns 1 when the flattened worlds agree (nodes,
+ * lists, primitives, roots, stack need: bit for bit), 0 when not, < 0 on an
+ * error.  The scene is not modified. */
+int32_t rt_world_selftest(rt_scene* s, int32_t world, int32_t lights, int32_t background_tex);
+
 /* ---- Multi-process communicator (RCCL) -------------------------------------- */
 #define RT_COMM_ID_BYTES 128
 /* ncclGetUniqueId: call on rank 0 and hand the bytes to every rank. */

@@ -127,14 +127,16 @@ SIGNATURES = {
     "world_info_get": (_I, [_P, _I, _I, _I, _U, C.POINTER(RtWorldInfo)]),
     "render_partials_get": (_I, [_P, _DP, C.c_uint64]),
     "math_selftest": (_I, [_I, _I, _DP, _DP, _DP, C.c_uint64]),
+    "bvh_selftest": (_I, [_P, _I]),
+    "world_selftest": (_I, [_P, _I, _I, _I]),
     "comm_unique_id": (_I, [C.POINTER(C.c_uint8)]),
     "comm_init": (_P, [C.POINTER(C.c_uint8), _I, _I]),
     "comm_destroy": (None, [_P]),
 }
 
-# Entry points of the GPU library only (the oracle renders on host cores and
-# has no communicator or device-side partial sums).
-GPU_ONLY = ("render_partials_get", "math_selftest", "comm_unique_id", "comm_init", "comm_destroy")
+# Entry points of the product library only (the oracle renders on host cores
+# and has no communicator, device-side partial sums or parallel builders).
+GPU_ONLY = ("render_partials_get", "math_selftest", "bvh_selftest", "world_selftest", "comm_unique_id", "comm_init", "comm_destroy")
 
 # Entry points only a CPU implementation has (the oracle).
 ORACLE_EXTRAS = {

@@ -17,8 +17,11 @@
 //  - each triangle's material is a RemappedMaterial (obj.rs:20-81): the
 //    shading normal is the normalised barycentric mix of the vertex normals and
 //    (u, v) become texture coordinates.
+#include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -118,21 +121,81 @@ std::vector<double> params(const MtlRec& m, const char* key) {
     }
     return v;
 }
+struct Corner {
+    int64_t v, t, n;
+    bool operator==(const Corner& o) const { return v == o.v && t == o.t && n == o.n; }
+};
+struct CornerHash {
+    size_t operator()(const Corner& c) const {
+        uint64_t h = (uint64_t)c.v * 0x9E3779B97F4A7C15ull;
+        h ^= (uint64_t)c.t + 0x632BE59BD9B4E019ull + (h << 6) + (h >> 2);
+        h ^= (uint64_t)c.n + 0x85EBCA77C2B2AE63ull + (h << 6) + (h >> 2);
+        return (size_t)h;
+    }
+};
 struct Model {
     std::string name;
     int material_id = -1;
     std::vector<int64_t> pos, tex, nrm;  // per single-index vertex: source indices
     std::vector<uint32_t> indices;       // triangles
-    std::map<std::tuple<int64_t, int64_t, int64_t>, uint32_t> vmap;
+    std::unordered_map<Corner, uint32_t, CornerHash> vmap;  // (v, vt, vn) -> vertex, first use numbers it
 };
+
+// The whitespace-separated words of one line, in place: each word is
+// NUL-terminated in the (mutable) line buffer.
+struct Words {
+    char* p;
+    char* end;
+    char* next() {
+        while (p < end && (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\f' || *p == '\v')) ++p;
+        if (p >= end) return nullptr;
+        char* w = p;
+        while (p < end && !(*p == ' ' || *p == '\t' || *p == '\r' || *p == '\f' || *p == '\v')) ++p;
+        if (p < end) *p++ = 0;
+        else *p = 0;  // the buffer keeps one byte past every line
+        return w;
+    }
+    // the rest of the line, trimmed
+    std::string rest() {
+        while (p < end && (*p == ' ' || *p == '\t')) ++p;
+        char* e = end;
+        while (e > p && (e[-1] == ' ' || e[-1] == '\t' || e[-1] == '\r' || e[-1] == '\f' || e[-1] == '\v')) --e;
+        return std::string(p, (size_t)(e - p));
+    }
+};
+// f64::from_str on one word: the whole word must parse
+bool parse_f64(const char* w, double& x) {
+    if (!w) return false;
+    char* e = nullptr;
+    x = std::strtod(w, &e);
+    return e != w && *e == 0;
+}
+// a face index (std::stoll semantics: leading digits, error when there are none)
+int64_t parse_index(const char* b, const char* e) {
+    char buf[32];
+    const size_t n = std::min<size_t>((size_t)(e - b), sizeof buf - 1);
+    std::memcpy(buf, b, n);
+    buf[n] = 0;
+    char* end = nullptr;
+    errno = 0;
+    const long long v = std::strtoll(buf, &end, 10);
+    if (end == buf) throw std::invalid_argument("face index '" + std::string(buf) + "'");
+    if (errno == ERANGE) throw std::out_of_range("face index '" + std::string(buf) + "'");
+    return v;
+}
 
 }  // namespace
 
 extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t vanilla) {
     if (!s || !obj_path) return set_error(RT_EINVAL, "null argument");
     try {
-        std::ifstream f(obj_path);
+        std::ifstream f(obj_path, std::ios::binary);
         if (!f) return set_error(RT_EINVAL, std::string("cannot open OBJ ") + obj_path);
+        // the whole file, parsed in place line by line (1M-triangle OBJs: a
+        // stream extraction per word took ~3 s)
+        std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        text.push_back('\n');
+        text.push_back(0);
         std::string path(obj_path);
         std::string dir = path.find('/') == std::string::npos ? "." : path.substr(0, path.rfind('/'));
         std::vector<double> P, T, N;  // v / vt / vn
@@ -152,42 +215,42 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
             }
         };
         auto resolve = [](int64_t i, size_t n) -> int64_t { return i < 0 ? (int64_t)n + i : i - 1; };
-        std::string line;
-        while (std::getline(f, line)) {
-            size_t c = line.find('#');
-            if (c != std::string::npos) line.resize(c);
-            line = trim(line);
-            if (line.empty()) continue;
-            std::istringstream is(line);
-            std::string key;
-            is >> key;
-            if (key == "v") {
-                double x, y, z;
-                is >> x >> y >> z;
-                P.insert(P.end(), {x, y, z});
-            } else if (key == "vt") {
-                double u = 0, v = 0;
-                is >> u >> v;
-                T.insert(T.end(), {u, v});
-            } else if (key == "vn") {
-                double x, y, z;
-                is >> x >> y >> z;
-                N.insert(N.end(), {x, y, z});
-            } else if (key == "o" || key == "g") {
-                std::string rest;
-                std::getline(is, rest);
-                finish_model(trim(rest));
-            } else if (key == "mtllib") {
-                std::string rest;
-                std::getline(is, rest);
+        std::vector<uint32_t> face;
+        char* const text_end = &text[text.size() - 1];  // the final NUL
+        for (char* line = &text[0]; line < text_end;) {
+            char* eol = (char*)std::memchr(line, '\n', (size_t)(text_end - line));
+            if (!eol) eol = text_end;
+            char* next_line = eol + 1;
+            char* hash = (char*)std::memchr(line, '#', (size_t)(eol - line));
+            Words is{line, hash ? hash : eol};
+            line = next_line;
+            const char* key = is.next();
+            if (!key) continue;
+            if (key[0] == 'v' && (key[1] == 0 || (key[2] == 0 && (key[1] == 't' || key[1] == 'n')))) {
+                double x[3] = {0, 0, 0};
+                if (key[1] == 't') {  // vt u [v]: missing values read as 0
+                    double u;
+                    if (parse_f64(is.next(), u)) {
+                        x[0] = u;
+                        if (parse_f64(is.next(), u)) x[1] = u;
+                    }
+                    T.insert(T.end(), {x[0], x[1]});
+                    continue;
+                }
+                for (int k = 0; k < 3; ++k)
+                    if (!parse_f64(is.next(), x[k]))  // tobj: PositionParseError / NormalParseError
+                        return set_error(RT_EPANIC, std::string("OBJ ") + (key[1] ? "normal" : "position") +
+                                                        " parse error (Wavefont::new expects the load to succeed)");
+                (key[1] ? N : P).insert((key[1] ? N : P).end(), {x[0], x[1], x[2]});
+            } else if (!std::strcmp(key, "o") || !std::strcmp(key, "g")) {
+                finish_model(is.rest());
+            } else if (!std::strcmp(key, "mtllib")) {
                 std::string err;
-                if (!parse_mtl(dir + "/" + trim(rest), mtls, err)) mtl_failed = true;
+                if (!parse_mtl(dir + "/" + is.rest(), mtls, err)) mtl_failed = true;
                 mtl_index.clear();
                 for (size_t i = 0; i < mtls.size(); ++i) mtl_index[mtls[i].name] = (int)i;
-            } else if (key == "usemtl") {
-                std::string rest;
-                std::getline(is, rest);
-                auto it = mtl_index.find(trim(rest));
+            } else if (!std::strcmp(key, "usemtl")) {
+                auto it = mtl_index.find(is.rest());
                 int id = it == mtl_index.end() ? -1 : it->second;
                 Model& cur = models.back();
                 if (!cur.indices.empty() && cur.material_id != id) {
@@ -196,33 +259,28 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
                     models.push_back(std::move(nm));
                 }
                 models.back().material_id = id;
-            } else if (key == "f") {
-                std::vector<uint32_t> face;
-                std::string tok;
+            } else if (!std::strcmp(key, "f")) {
+                face.clear();
                 Model& m = models.back();
-                while (is >> tok) {
-                    int64_t vi = 0, ti = INT64_MIN, ni = INT64_MIN;
-                    size_t a = tok.find('/');
-                    vi = resolve(std::stoll(tok.substr(0, a)), P.size() / 3);
-                    if (a != std::string::npos) {
-                        size_t b = tok.find('/', a + 1);
-                        std::string ts = tok.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
-                        if (!ts.empty()) ti = resolve(std::stoll(ts), T.size() / 2);
-                        if (b != std::string::npos && b + 1 < tok.size()) ni = resolve(std::stoll(tok.substr(b + 1)), N.size() / 3);
+                while (const char* tok = is.next()) {
+                    int64_t ti = INT64_MIN, ni = INT64_MIN;
+                    const char* tend = tok + std::strlen(tok);
+                    const char* a = std::strchr(tok, '/');
+                    const int64_t vi = resolve(parse_index(tok, a ? a : tend), P.size() / 3);
+                    if (a) {
+                        const char* b = std::strchr(a + 1, '/');
+                        const char* te = b ? b : tend;
+                        if (te > a + 1) ti = resolve(parse_index(a + 1, te), T.size() / 2);
+                        if (b && b + 1 < tend) ni = resolve(parse_index(b + 1, tend), N.size() / 3);
                     }
-                    auto key3 = std::make_tuple(vi, ti, ni);
-                    auto it = m.vmap.find(key3);
-                    uint32_t idx;
-                    if (it == m.vmap.end()) {
-                        idx = (uint32_t)m.pos.size();
-                        m.vmap.emplace(key3, idx);
+                    const Corner key3{vi, ti, ni};
+                    auto ins = m.vmap.emplace(key3, (uint32_t)m.pos.size());
+                    if (ins.second) {
                         m.pos.push_back(vi);
                         m.tex.push_back(ti);
                         m.nrm.push_back(ni);
-                    } else {
-                        idx = it->second;
                     }
-                    face.push_back(idx);
+                    face.push_back(ins.first->second);
                 }
                 for (size_t i = 1; i + 1 < face.size(); ++i) m.indices.insert(m.indices.end(), {face[0], face[i], face[i + 1]});
             }
@@ -316,6 +374,11 @@ extern "C" int32_t rt_wavefront_load(rt_scene* s, const char* obj_path, int32_t 
         int32_t objs = rt_hittables_new(s);
         const int32_t empty = mats.empty() ? -1 : rt_mat_empty(s);
         const size_t nload = std::min(models.size(), mtls.size());  // zip (obj.rs:129)
+        {  // room for every triangle and its model's BVH nodes (about one per triangle) up front
+            size_t ntri = 0;
+            for (size_t mi = 0; mi < nload; ++mi) ntri += models[mi].indices.size() / 3;
+            s->objs.reserve(s->objs.size() + 2 * ntri + 2 * nload + 1);
+        }
         for (size_t mi = 0; mi < nload; ++mi) {
             const Model& m = models[mi];
             int32_t list = rt_hittables_new(s);

@@ -7,8 +7,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <limits>
+#include <thread>
 #include <unordered_map>
 
 #include "../../include/rt_mi355x.h"
@@ -26,6 +28,8 @@ int32_t set_error(int32_t code, const std::string& msg) {
 }
 
 static const double INF = std::numeric_limits<double>::infinity();
+// rt_world_selftest: this thread's flattens build their BVHs serially
+static thread_local bool g_serial_build = false;
 
 // aabb.rs:43-51 pad_to_minimums, interval.rs:28-34 expand, 44-46 size
 static Iv pad(Iv t) {
@@ -78,8 +82,99 @@ static bool total_less(double a, double b) {
     return ia < ib;
 }
 
-// bvh.rs:16-46 -- returns the object id of the new BVH node
-static int bvh_from_vec(rt_scene* s, std::vector<int> objects) {
+// bvh.rs:16-46, restated over a compact (box, id) array and built in
+// parallel, node for node the tree and the object ids of bvh_from_vec_serial
+// below (kept as the statement of the recursion): a call makes one node, its
+// left subtree's nodes first, then its right subtree's, then itself (post
+// order), so the ids of a subtree of n objects are a block of
+// bvh_node_count(n) ids fixed by n alone and both halves can be filled at
+// once.  1M-triangle OBJ models: ~3 s per model serial, mostly cache misses
+// of the comparator reading each object's box.
+namespace {
+struct BvhItem {
+    Box3 box;
+    int id;
+};
+size_t bvh_node_count(size_t n) {
+    // nodes for n objects: one per call, a call on <= 2 objects is a leaf
+    // node; sizes at one depth are floor / ceil of one quotient, so few
+    // distinct n come up
+    static thread_local std::unordered_map<size_t, size_t> memo;
+    if (n <= 2) return 1;
+    auto it = memo.find(n);
+    if (it != memo.end()) return it->second;
+    const size_t c = 1 + bvh_node_count(n / 2) + bvh_node_count(n - n / 2);
+    memo.emplace(n, c);
+    return c;
+}
+void bvh_build(rt_scene* s, BvhItem* it, size_t len, size_t base, int par) {
+    Box3 bbox = Box3::empty();
+    for (size_t i = 0; i < len; ++i) bbox = bbox.unite(it[i].box);  // the same order as the serial loop
+    const int axis = bbox.longest_axis();
+    Obj node;
+    node.kind = O_BVH;
+    node.hidden = true;
+    node.bbox = bbox;
+    size_t self = base;
+    if (len == 1) {
+        node.left = it[0].id;
+    } else if (len == 2) {
+        node.left = it[0].id;
+        node.right = it[1].id;
+    } else {
+        // the stable sort on (key, position) pairs, then one gather: a third
+        // of the bytes a sort of the 56-B items moves
+        {
+            std::vector<std::pair<int64_t, uint32_t>> kp(len);
+            for (size_t i = 0; i < len; ++i) {
+                int64_t k;
+                std::memcpy(&k, &it[i].box.a[axis].lo, 8);
+                k ^= (int64_t)(((uint64_t)(k >> 63)) >> 1);  // total_less's order as integers
+                kp[i] = {k, (uint32_t)i};
+            }
+            std::stable_sort(kp.begin(), kp.end(),
+                             [](const std::pair<int64_t, uint32_t>& a, const std::pair<int64_t, uint32_t>& b) {
+                                 return a.first < b.first;
+                             });
+            std::vector<BvhItem> tmp(it, it + len);
+            for (size_t i = 0; i < len; ++i) it[i] = tmp[kp[i].second];
+        }
+        const size_t mid = len / 2, nl = bvh_node_count(mid), nr = bvh_node_count(len - mid);
+        node.left = (int)(base + nl - 1);  // a subtree's root is its last node
+        node.right = (int)(base + nl + nr - 1);
+        if (par > 0 && len >= 16384) {
+            std::exception_ptr err;
+            std::thread t([&] {
+                try {
+                    bvh_build(s, it, mid, base, par - 1);
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            });
+            bvh_build(s, it + mid, len - mid, base + nl, par - 1);
+            t.join();
+            if (err) std::rethrow_exception(err);
+        } else {
+            bvh_build(s, it, mid, base, 0);
+            bvh_build(s, it + mid, len - mid, base + nl, 0);
+        }
+        self = base + nl + nr;
+    }
+    s->objs[self] = std::move(node);
+}
+}  // namespace
+static int bvh_from_vec(rt_scene* s, const std::vector<int>& objects) {
+    std::vector<BvhItem> items(objects.size());
+    for (size_t i = 0; i < objects.size(); ++i) items[i] = BvhItem{s->objs[objects[i]].bbox, objects[i]};
+    const size_t base = s->objs.size(), n = bvh_node_count(objects.size());
+    s->objs.resize(base + n);
+    bvh_build(s, items.data(), items.size(), base, 4);  // up to 16 threads
+    return (int)(base + n - 1);
+}
+
+// bvh.rs:16-46 -- returns the object id of the new BVH node (the serial
+// recursion; tests/test_tiers_cpu.py checks bvh_from_vec against it)
+int bvh_from_vec_serial(rt_scene* s, std::vector<int> objects) {
     Box3 bbox = Box3::empty();
     for (int o : objects) bbox = bbox.unite(s->objs[o].bbox);
     int axis = bbox.longest_axis();
@@ -99,8 +194,8 @@ static int bvh_from_vec(rt_scene* s, std::vector<int> objects) {
         });
         size_t mid = len / 2;
         std::vector<int> lv(objects.begin(), objects.begin() + mid), rv(objects.begin() + mid, objects.end());
-        node.left = bvh_from_vec(s, std::move(lv));
-        node.right = bvh_from_vec(s, std::move(rv));
+        node.left = bvh_from_vec_serial(s, std::move(lv));
+        node.right = bvh_from_vec_serial(s, std::move(rv));
     }
     s->objs.push_back(node);
     return (int)s->objs.size() - 1;
@@ -168,9 +263,19 @@ struct Flattener {
     // for Hittables built from Hittables::default() (hits.rs:9, aabb.rs:9); the
     // SAH build uses these tight ones instead.
     Box3 tight(int id) {
+        const Obj& o = s->objs[id];
+        // primitives: their own box; a BVH's inner nodes are reached only
+        // through their parent (objects are moved, never shared): neither is
+        // worth a memo entry (1M-triangle meshes: two million of them)
+        if (o.kind != O_LIST && o.kind != O_BVH && o.kind != O_XFORM && o.kind != O_MEDIUM) return o.bbox;
+        if (o.kind == O_BVH && o.hidden) {
+            Box3 b = Box3::empty();
+            if (o.left >= 0) b = b.unite(tight(o.left));
+            if (o.right >= 0) b = b.unite(tight(o.right));
+            return b;
+        }
         auto it = tight_memo.find(id);
         if (it != tight_memo.end()) return it->second;
-        const Obj& o = s->objs[id];
         Box3 b = o.bbox;
         switch (o.kind) {
             case O_LIST:
@@ -241,10 +346,47 @@ struct Flattener {
         double c[3];
     };
 
+    // Nodes of a subtree under construction: refs to nodes made by the same
+    // build are relative to `n` (flag `local`), every other ref (the items'
+    // own: primitives, nested BVHs already in out.nodes) is final.
+    struct NodeBuf {
+        std::vector<rtk::DNode> n;
+        std::vector<uint8_t> local;  // bit 0: c0 is a node of this build, bit 1: c1
+        // appends `sub` (its local refs rebased by where it lands); returns that offset
+        uint32_t splice(const NodeBuf& sub) {
+            const uint32_t off = (uint32_t)n.size();
+            n.insert(n.end(), sub.n.begin(), sub.n.end());
+            local.insert(local.end(), sub.local.begin(), sub.local.end());
+            for (size_t k = off; k < n.size(); ++k) {
+                if (local[k] & 1u) n[k].c0 += off;  // (index field only: no carry into the kind)
+                if (local[k] & 2u) n[k].c1 += off;
+            }
+            return off;
+        }
+    };
+    struct Built {
+        uint32_t ref, need;
+        bool local;
+    };
     // Binned SAH (32 bins x 3 axes) over items[b, e); leaves hold one object,
-    // the parent carries each child's box.  Returns (ref, need).
+    // the parent carries each child's box.  Returns (ref, need).  Nodes are
+    // numbered in preorder (a node, its left subtree, its right subtree); the
+    // two halves of a large node are built at once into their own buffers and
+    // spliced in that order, so the tree and its numbering do not depend on
+    // the threads (1M-triangle OBJ models: ~1.3 s per model serial).
     std::pair<uint32_t, uint32_t> sah(std::vector<Item>& it, size_t b, size_t e) {
-        if (e - b == 1) return {it[b].ref, it[b].need};
+        NodeBuf nb;
+        const Built r = sah_build(it, b, e, nb, g_serial_build ? 0 : 4);  // up to 16 threads
+        const uint32_t off = (uint32_t)out.nodes.size();
+        out.nodes.insert(out.nodes.end(), nb.n.begin(), nb.n.end());
+        for (size_t k = 0; k < nb.n.size(); ++k) {
+            if (nb.local[k] & 1u) out.nodes[off + k].c0 += off;
+            if (nb.local[k] & 2u) out.nodes[off + k].c1 += off;
+        }
+        return {r.local ? r.ref + off : r.ref, r.need};
+    }
+    Built sah_build(std::vector<Item>& it, size_t b, size_t e, NodeBuf& nb, int par) {
+        if (e - b == 1) return {it[b].ref, it[b].need, false};
         size_t mid = b + (e - b) / 2;
         double cmin[3], cmax[3];
         for (int k = 0; k < 3; ++k) {
@@ -306,20 +448,42 @@ struct Flattener {
             mid = (size_t)(pivot - it.begin());
             if (mid == b || mid == e) mid = b + (e - b) / 2;
         }
-        uint32_t idx = (uint32_t)out.nodes.size();
-        out.nodes.emplace_back();
-        auto L = sah(it, b, mid);
-        auto R = sah(it, mid, e);
+        const uint32_t idx = (uint32_t)nb.n.size();
+        nb.n.emplace_back();
+        nb.local.push_back(0);
+        Built L, R;
+        if (par > 0 && e - b >= 32768) {
+            NodeBuf lb, rb;
+            std::exception_ptr err;
+            std::thread t([&] {
+                try {
+                    L = sah_build(it, b, mid, lb, par - 1);
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            });
+            R = sah_build(it, mid, e, rb, par - 1);
+            t.join();
+            if (err) std::rethrow_exception(err);
+            const uint32_t offl = nb.splice(lb);
+            if (L.local) L.ref += offl;
+            const uint32_t offr = nb.splice(rb);
+            if (R.local) R.ref += offr;
+        } else {
+            L = sah_build(it, b, mid, nb, 0);
+            R = sah_build(it, mid, e, nb, 0);
+        }
         Box3 bl = Box3::empty(), br = Box3::empty();
         for (size_t i = b; i < mid; ++i) bl = bl.unite(it[i].box);
         for (size_t i = mid; i < e; ++i) br = br.unite(it[i].box);
-        rtk::DNode& n = out.nodes[idx];
-        set_child(n, 0, L.first, bl);
-        set_child(n, 1, R.first, br);
-        n.c0 = L.first;
-        n.c1 = R.first;
+        rtk::DNode& n = nb.n[idx];
+        set_child(n, 0, L.ref, bl);
+        set_child(n, 1, R.ref, br);
+        n.c0 = L.ref;
+        n.c1 = R.ref;
+        nb.local[idx] = (L.local ? 1u : 0u) | (R.local ? 2u : 0u);
         // near-first: the far child waits on the stack while the near one is walked
-        return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.second, R.second)};
+        return {rtk::make_ref(rtk::K_BVH, idx), 1 + std::max(L.need, R.need), true};
     }
 
     // Reference topology (bvh.rs:16-46) in the two-box node format.
@@ -1141,6 +1305,53 @@ int32_t rt_bvh_new(rt_scene* s, int32_t list) {
     s->objs[root].hidden = false;
     ++s->generation;
     return root;
+}
+int32_t rt_bvh_selftest(rt_scene* s, int32_t list) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    int32_t rc;
+    if ((rc = check_obj(s, list)) != RT_OK) return rc;
+    if (s->objs[list].kind != O_LIST || s->objs[list].children.empty())
+        return set_error(RT_EHANDLE, "not a non-empty Hittables object");
+    try {
+        rt_scene a, b;
+        a.objs = s->objs;
+        b.objs = s->objs;
+        const int ra = bvh_from_vec(&a, s->objs[list].children);
+        const int rb = bvh_from_vec_serial(&b, s->objs[list].children);
+        if (ra != rb || a.objs.size() != b.objs.size()) return 0;
+        for (size_t i = s->objs.size(); i < a.objs.size(); ++i) {
+            const Obj &x = a.objs[i], &y = b.objs[i];
+            if (x.kind != y.kind || x.left != y.left || x.right != y.right || x.hidden != y.hidden ||
+                std::memcmp(&x.bbox, &y.bbox, sizeof(Box3)) != 0)
+                return 0;
+        }
+        return 1;
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
+}
+int32_t rt_world_selftest(rt_scene* s, int32_t world, int32_t lights, int32_t background_tex) {
+    if (!s) return set_error(RT_EINVAL, "null argument");
+    try {
+        HostWorld p, q;
+        int32_t rc = flatten(s, world, lights, background_tex, false, p);
+        if (rc != RT_OK) return rc;
+        g_serial_build = true;
+        rc = flatten(s, world, lights, background_tex, false, q);
+        g_serial_build = false;
+        if (rc != RT_OK) return rc;
+        auto same = [](const auto& x, const auto& y) {
+            return x.size() == y.size() && (x.empty() || std::memcmp(x.data(), y.data(), x.size() * sizeof(x[0])) == 0);
+        };
+        return (same(p.nodes, q.nodes) && same(p.list_children, q.list_children) && same(p.planars, q.planars) &&
+                same(p.spheres, q.spheres) && p.world_root == q.world_root && p.lights_root == q.lights_root &&
+                p.stack_need == q.stack_need)
+                   ? 1
+                   : 0;
+    } catch (const std::bad_alloc&) {
+        g_serial_build = false;
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
 }
 int32_t rt_build_box(rt_scene* s, const double a[3], const double b[3], int32_t mat) {
     if (!s || bad(a) || bad(b)) return set_error(RT_EINVAL, "null argument");
