@@ -1650,13 +1650,14 @@ void bvh4_relayout(HostWorld& hw, int mode) {
     const size_t n = hw.nodes4.size();
     // new position of each node: a node's inner children get consecutive
     // slots (so the siblings a walk pops are neighbours), depth first
-    std::vector<uint32_t> at(n, REF_NONE), order;
+    constexpr uint32_t UNSET = UINT32_MAX;  // (REF_NONE is 0: a valid position)
+    std::vector<uint32_t> at(n, UNSET), order;
     order.reserve(n);
     std::vector<uint32_t> todo;
     auto place = [&](uint32_t ref) {
         if (rtk::ref_kind(ref) != rtk::K_BVH) return false;
         const uint32_t i = rtk::ref_index(ref);
-        if (i >= n || at[i] != REF_NONE) return false;
+        if (i >= n || at[i] != UNSET) return false;
         at[i] = (uint32_t)order.size();
         order.push_back(i);
         return true;
@@ -1691,6 +1692,49 @@ void bvh4_relayout(HostWorld& hw, int mode) {
     for (uint32_t& r : hw.list_children) r = remap(r);
     for (rtk::DXform& x : hw.xforms) x.child = remap(x.child);
     for (rtk::DMedium& m : hw.media) m.boundary = remap(m.boundary);
+    // mode 2: the quad / triangle records in the order the nodes name them,
+    // so a leaf node's primitives share lines.  Media name their boundary
+    // quads as a range (DMedium::planar_first): worlds with media keep theirs.
+    if (mode < 2 || !hw.media.empty() || hw.planars.empty()) return;
+    const size_t np = hw.planars.size();
+    std::vector<uint32_t> pat(np, UNSET), porder;
+    porder.reserve(np);
+    auto pplace = [&](uint32_t r) {
+        const uint32_t k = rtk::ref_kind(r);
+        if (k != rtk::K_QUAD && k != rtk::K_TRI) return;
+        const uint32_t i = rtk::ref_index(r);
+        if (i < np && pat[i] == UNSET) {
+            pat[i] = (uint32_t)porder.size();
+            porder.push_back(i);
+        }
+    };
+    for (const rtk::DNode4& nd : hw.nodes4)
+        for (int s = 0; s < 4; ++s) pplace(nd.ref[s]);
+    for (uint32_t i = 0; i < np; ++i)
+        if (pat[i] == UNSET) {
+            pat[i] = (uint32_t)porder.size();
+            porder.push_back(i);
+        }
+    auto permute = [&](auto& v) {
+        if (v.size() != np) return;
+        auto old = v;
+        for (size_t k = 0; k < np; ++k) v[k] = old[porder[k]];
+    };
+    permute(hw.planars);
+    permute(hw.planars_f);
+    permute(hw.planar_area);
+    permute(hw.planar_mat);
+    permute(hw.planar_remap);
+    auto premap = [&](uint32_t r) {
+        const uint32_t k = rtk::ref_kind(r);
+        return (k == rtk::K_QUAD || k == rtk::K_TRI) ? rtk::make_ref(k, pat[rtk::ref_index(r)]) : r;
+    };
+    for (rtk::DNode4& nd : hw.nodes4)
+        for (int s = 0; s < 4; ++s) nd.ref[s] = premap(nd.ref[s]);
+    hw.world_root = premap(hw.world_root);
+    hw.lights_root = premap(hw.lights_root);
+    for (uint32_t& r : hw.list_children) r = premap(r);
+    for (rtk::DXform& x : hw.xforms) x.child = premap(x.child);
 }
 
 bool bvh4_quantize(HostWorld& hw) {

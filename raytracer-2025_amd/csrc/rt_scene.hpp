@@ -167,8 +167,10 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes = SIZE_MAX);
 // Re-lays out the 4-wide nodes of a converted world (same topology, refs
 // rewritten): mode 0 keeps the build's depth-first order; 1 places a node's
-// inner children consecutively (depth first over the sibling groups).
-// Measured without effect: an A/B option, default 0.
+// inner children consecutively (depth first over the sibling groups); 2
+// also stores the quad / triangle records in the order the nodes name them
+// (worlds without media).  Measured without effect: an
+// A/B option, default 0.
 #ifndef RT_BVH4_LAYOUT
 #define RT_BVH4_LAYOUT 0
 #endif
