@@ -10,6 +10,7 @@
 #include <exception>
 #include <functional>
 #include <limits>
+#include <system_error>
 #include <thread>
 #include <unordered_map>
 
@@ -142,18 +143,29 @@ void bvh_build(rt_scene* s, BvhItem* it, size_t len, size_t base, int par) {
         const size_t mid = len / 2, nl = bvh_node_count(mid), nr = bvh_node_count(len - mid);
         node.left = (int)(base + nl - 1);  // a subtree's root is its last node
         node.right = (int)(base + nl + nr - 1);
+        std::thread t;
+        std::exception_ptr err;
         if (par > 0 && len >= 16384) {
-            std::exception_ptr err;
-            std::thread t([&] {
-                try {
-                    bvh_build(s, it, mid, base, par - 1);
-                } catch (...) {
-                    err = std::current_exception();
-                }
-            });
-            bvh_build(s, it + mid, len - mid, base + nl, par - 1);
-            t.join();
-            if (err) std::rethrow_exception(err);
+            try {
+                t = std::thread([&] {
+                    try {
+                        bvh_build(s, it, mid, base, par - 1);
+                    } catch (...) {
+                        err = std::current_exception();
+                    }
+                });
+            } catch (const std::system_error&) {  // no thread to be had: this one builds both
+            }
+        }
+        if (t.joinable()) {
+            std::exception_ptr err_r;
+            try {
+                bvh_build(s, it + mid, len - mid, base + nl, par - 1);
+            } catch (...) {
+                err_r = std::current_exception();
+            }
+            t.join();  // before anything leaves this frame
+            if (err || err_r) std::rethrow_exception(err ? err : err_r);
         } else {
             bvh_build(s, it, mid, base, 0);
             bvh_build(s, it + mid, len - mid, base + nl, 0);
@@ -168,7 +180,12 @@ static int bvh_from_vec(rt_scene* s, const std::vector<int>& objects) {
     for (size_t i = 0; i < objects.size(); ++i) items[i] = BvhItem{s->objs[objects[i]].bbox, objects[i]};
     const size_t base = s->objs.size(), n = bvh_node_count(objects.size());
     s->objs.resize(base + n);
-    bvh_build(s, items.data(), items.size(), base, 4);  // up to 16 threads
+    try {
+        bvh_build(s, items.data(), items.size(), base, 4);  // up to 16 threads
+    } catch (...) {
+        s->objs.resize(base);  // no half-built nodes left behind
+        throw;
+    }
     return (int)(base + n - 1);
 }
 
@@ -452,19 +469,30 @@ struct Flattener {
         nb.n.emplace_back();
         nb.local.push_back(0);
         Built L, R;
+        NodeBuf lb, rb;
+        std::thread t;
+        std::exception_ptr err;
         if (par > 0 && e - b >= 32768) {
-            NodeBuf lb, rb;
-            std::exception_ptr err;
-            std::thread t([&] {
-                try {
-                    L = sah_build(it, b, mid, lb, par - 1);
-                } catch (...) {
-                    err = std::current_exception();
-                }
-            });
-            R = sah_build(it, mid, e, rb, par - 1);
-            t.join();
-            if (err) std::rethrow_exception(err);
+            try {
+                t = std::thread([&] {
+                    try {
+                        L = sah_build(it, b, mid, lb, par - 1);
+                    } catch (...) {
+                        err = std::current_exception();
+                    }
+                });
+            } catch (const std::system_error&) {  // no thread to be had: this one builds both
+            }
+        }
+        if (t.joinable()) {
+            std::exception_ptr err_r;
+            try {
+                R = sah_build(it, mid, e, rb, par - 1);
+            } catch (...) {
+                err_r = std::current_exception();
+            }
+            t.join();  // before anything leaves this frame
+            if (err || err_r) std::rethrow_exception(err ? err : err_r);
             const uint32_t offl = nb.splice(lb);
             if (L.local) L.ref += offl;
             const uint32_t offr = nb.splice(rb);
@@ -1299,9 +1327,13 @@ int32_t rt_bvh_new(rt_scene* s, int32_t list) {
     if ((rc = check_obj(s, list)) != RT_OK) return rc;
     if (s->objs[list].kind != O_LIST) return set_error(RT_EHANDLE, "not a Hittables object");
     if (s->objs[list].children.empty()) return set_error(RT_EPANIC, "BVH node must contain at least one object");
-    std::vector<int> objs = s->objs[list].children;
+    int root;
+    try {
+        root = bvh_from_vec(s, s->objs[list].children);
+    } catch (const std::bad_alloc&) {
+        return set_error(RT_ENOMEM, "out of host memory");
+    }
     s->objs[list].moved = true;
-    int root = bvh_from_vec(s, std::move(objs));
     s->objs[root].hidden = false;
     ++s->generation;
     return root;
