@@ -21,7 +21,10 @@
  *  - Reference panics (assert!, expect, unwrap, unimplemented!) become
  *    RT_EPANIC with a message; the library never aborts the process.
  *  - Not thread-safe per scene: calls on one scene are serialised by the
- *    caller.  Different scenes may be used from different threads.
+ *    caller.  Different scenes may be used from different threads, also
+ *    when they render on the same device list or through the same rt_comm:
+ *    the frame gathers of such renders are enqueued one whole RCCL group
+ *    at a time.
  */
 #ifndef RT_MI355X_H
 #define RT_MI355X_H

@@ -11,6 +11,10 @@ from .capi import Api, RtError  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librt_mi355x.so")
+# RT_MI355X_LIB names another build of the same ABI for a whole test run (the
+# check build: `make -C raytracer-2025_amd check`, librt_mi355x_check.so)
+if os.environ.get("RT_MI355X_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["RT_MI355X_LIB"])
 
 _api = None
 

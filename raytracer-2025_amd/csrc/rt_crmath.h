@@ -335,26 +335,6 @@ RTCR_FN double cos(double x) {
     sincos_slow(x, &s, &c);
     return c;
 }
-// sincos with the table records read through `tab(k, S, C)` (the kernel's
-// basic tier keeps a copy of the table in LDS); the slow path reads the
-// global table
-template <class Tab>
-RTCR_FN void sincos_tab(double x, double* s, double* c, const Tab& tab) {
-    ScR p;
-    if (sc_prep(x, p)) {
-        DD S, C;
-        tab(p.k, S, C);
-        double ys, yc;
-        const bool oks = sc_combine(S, C, p.rh, p.rl, p.hq, p.cmr, p.t, ys);
-        const bool okc = sc_combine(C, dd_neg(S), p.rh, p.rl, p.hq, p.cmr, p.t, yc);
-        if (oks && okc) {
-            *s = ys;
-            *c = yc;
-            return;
-        }
-    }
-    sincos_slow(x, s, c);
-}
 RTCR_FN void sincos(double x, double* s, double* c) {
     ScR p;
     if (sc_prep(x, p)) {

@@ -20,7 +20,7 @@
 
 namespace rthdr {
 
-enum Status { OK = 0, CORRUPT = 2 };
+enum Status { OK = 0, CORRUPT = 2, UNSUPPORTED = 3 };  // UNSUPPORTED: a library limit
 
 inline float rgbe_channel(uint8_t c, uint8_t e) { return e ? std::ldexp((float)c, (int)e - 136) : 0.0f; }
 
@@ -58,9 +58,13 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
     long h = 0, w = 0;
     char ya[3] = {}, xa[3] = {};
     if (std::sscanf(s.c_str(), "%2s %ld %2s %ld", ya, &h, xa, &w) != 4 || std::strcmp(ya, "-Y") || std::strcmp(xa, "+X") ||
-        h <= 0 || w <= 0 || (uint64_t)h * (uint64_t)w > (1ull << 28)) {
+        h <= 0 || w <= 0) {
         err = "HDR orientation other than -Y h +X w";
         return CORRUPT;
+    }
+    if ((uint64_t)h * (uint64_t)w > (1ull << 28)) {
+        err = "HDR larger than this library's 2^28-pixel limit";
+        return UNSUPPORTED;
     }
     W = (uint32_t)w;
     H = (uint32_t)h;
@@ -100,10 +104,15 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
                 const uint8_t* p = &f[pos];
                 pos += 4;
                 if (p[0] == 1 && p[1] == 1 && p[2] == 1) {
-                    const uint64_t cnt = (uint64_t)p[3] << shift;
-                    if (!(ok = x > 0 && x + cnt <= W)) break;
+                    // the shift grows by 8 per consecutive repeat marker (Radiance's
+                    // oldreadcolrs); past 24 bits any nonzero count exceeds the
+                    // 2^28-pixel limit, so such a chain is corrupt (and a shift of
+                    // 64 would be undefined)
+                    if (!(ok = shift <= 24 || p[3] == 0)) break;
+                    const uint64_t cnt = shift <= 24 ? (uint64_t)p[3] << shift : 0u;
+                    if (!(ok = x > 0 && cnt <= W - x)) break;
                     for (uint64_t k = 0; k < cnt; ++k, ++x) std::memcpy(&row[(size_t)x * 4], &row[(size_t)(x - 1) * 4], 4);
-                    shift += 8;
+                    shift = shift < 32 ? shift + 8 : 32;
                 } else {
                     std::memcpy(&row[(size_t)(x++) * 4], p, 4);
                     shift = 0;

@@ -59,20 +59,24 @@ inline Status load(const std::string& path, bool raw, uint32_t& W, uint32_t& H, 
     size_t n;
     while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) f.insert(f.end(), buf, buf + n);
     std::fclose(fp);
+    // Each decoder returns 3 (UNSUPPORTED) for what this library does not
+    // decode -- a library limit (more than 2^28 pixels) or a coding process
+    // it leaves out -- which the crate might decode: RT_EUNSUPPORTED, never a
+    // cyan image; anything else that fails (a bad signature, a corrupt
+    // stream) is the crate's decode error -> Image::EMPTY.
     int st;
-    if (fmt == F_PNG) {
+    if (fmt == F_PNG)
         st = (int)rtpng::decode(f, W, H, rgba, err);
-        if (st == rtpng::UNSUPPORTED) st = rtpng::CORRUPT;  // not a PNG: the crate's decode fails -> EMPTY
-    } else if (fmt == F_JPEG) {
+    else if (fmt == F_JPEG)
         st = (int)rtjpeg::decode(f, W, H, rgba, err);
-        if (st == rtjpeg::UNSUPPORTED) {
-            err = path + ": " + err;
-            W = H = 0;
-            rgba.clear();
-            return UNSUPPORTED;
-        }
-    } else {
+    else
         st = (int)rthdr::decode(f, W, H, rgba, err);
+    static_assert((int)rtpng::UNSUPPORTED == 3 && (int)rtjpeg::UNSUPPORTED == 3 && (int)rthdr::UNSUPPORTED == 3, "");
+    if (st == 3) {
+        err = path + ": " + err;
+        W = H = 0;
+        rgba.clear();
+        return UNSUPPORTED;
     }
     if (st != 0) {  // ImageReader::decode().ok()? -> None -> Image::EMPTY
         W = H = 0;

@@ -38,11 +38,17 @@ struct Huff {
     uint8_t look_len[512] = {}, look_val[512] = {};
     int32_t maxcode[18] = {}, valptr[17] = {}, mincode[17] = {};
     uint8_t vals[256] = {};
-    bool build(const uint8_t counts[16], const uint8_t* v, int nv) {
+    // dc: a DC table, whose symbols are bit counts of a difference -- above 15
+    // they are rejected, as libjpeg's jpeg_make_d_derived_tbl does (a count
+    // above 32 would also be an undefined shift in Bits::get / extend)
+    bool build(const uint8_t counts[16], const uint8_t* v, int nv, bool dc) {
         int total = 0;
         for (int l = 0; l < 16; ++l) total += counts[l];
         if (total > 256 || total > nv) return false;
         std::memcpy(vals, v, (size_t)total);
+        if (dc)
+            for (int i = 0; i < total; ++i)
+                if (vals[i] > 15) return false;
         std::memset(look_len, 0, sizeof look_len);
         int32_t code = 0;
         int k = 0;
@@ -51,13 +57,16 @@ struct Huff {
             mincode[l] = code;
             const int n = counts[l - 1];
             for (int i = 0; i < n; ++i, ++code, ++k) {
+                // over-subscribed: checked per code, before the code's
+                // lookahead entries are written (code < 2^l keeps them
+                // inside the 512-entry tables)
+                if (code >= (1 << l)) return false;
                 if (l <= 9) {
                     const int lo = code << (9 - l), hi = (code + 1) << (9 - l);
                     for (int c = lo; c < hi; ++c) look_len[c] = (uint8_t)l, look_val[c] = vals[k];
                 }
             }
             maxcode[l] = n ? code - 1 : -1;
-            if (code > (1 << l)) return false;  // over-subscribed
             code <<= 1;
         }
         maxcode[17] = 0x7fffffff;
@@ -297,7 +306,7 @@ struct Decoder {
             for (int l = 0; l < 16; ++l) total += p[i + 1 + l];
             if (i + 17 + (size_t)total > len) return fail(CORRUPT, "short DHT");
             Huff& h = tc == 0 ? dc[th] : ac[th];
-            if (!h.build(p + i + 1, p + i + 17, total)) return fail(CORRUPT, "bad Huffman table");
+            if (!h.build(p + i + 1, p + i + 17, total, tc == 0)) return fail(CORRUPT, "bad Huffman table");
             i += 17 + (size_t)total;
         }
         return OK;

@@ -105,7 +105,6 @@ struct rtk_frame_desc {
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need);
 extern "C" uint32_t rtk_stack_entries(int tier);
 // 1 if the basic tier's kernel walks 4-wide BVH nodes (rth::bvh4_basic)
-extern "C" int rtk_qnodes(void);
 extern "C" int rtk_basic_bvh4(void);
 // 1 if the mesh tier's kernel walks 4-wide BVH nodes with every child boxed
 extern "C" int rtk_mesh_bvh4(void);

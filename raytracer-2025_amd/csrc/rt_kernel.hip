@@ -22,7 +22,6 @@
 #include "rt_crmath.h"
 #include "rt_kernel.h"
 #include "rt_math.h"
-#include "rt_qnode.h"
 #include "rt_slab.h"
 #include "rt_sphere_filter.h"
 
@@ -40,14 +39,6 @@ namespace rtk {
 // Mesh tier: 4-wide BVH nodes with every child boxed (visit4_boxes).
 #ifndef RT_MESH_BVH4
 #define RT_MESH_BVH4 1
-#endif
-// Mesh / full tiers: 64-B nodes with 8-bit quantized child boxes (DNode4Q)
-// when the world's bounds allow (rt_render.cpp prepare_tier).  Off: measured
-// slower (A/B at 64 spp, 3 reps, RMSE 0: C4 53.8 -> 57.4 ms, C5 172.4 ->
-// 180.5 ms) -- the decode's ~50 VALU instructions per node visit cost more
-// than the three dwordx4 loads they save.
-#ifndef RT_QNODES
-#define RT_QNODES 0
 #endif
 // Full tier: the same boxed 4-wide nodes, for the walk and the medium boundary walks.
 #ifndef RT_FULL_BVH4
@@ -117,37 +108,37 @@ struct Frame {
     D3 center, pixel00, du, dv, disk_u, disk_v;
 };
 
-#ifndef RT_SC_LDS
-// basic tier: the correctly rounded sincos reads its sin / cos (k pi/128)
-// records from an LDS copy of the table (8 KiB) instead of global memory
-#define RT_SC_LDS 0
-#endif
-#if RT_SC_LDS
-__shared__ double g_sc_lds[256 * 4];
-struct ScTabLds {
-    __device__ __forceinline__ void operator()(int k, rtcr::DD& S, rtcr::DD& C) const {
-        const uint32_t i = (uint32_t)(k & 255) * 4u;
-        S = rtcr::DD{g_sc_lds[i], g_sc_lds[i + 1]};
-        C = rtcr::DD{g_sc_lds[i + 2], g_sc_lds[i + 3]};
-    }
-};
-#endif
-template <int TIER>
-__device__ __forceinline__ void t_sincos(double x, double* s, double* c) {
-#if RT_SC_LDS
-    if constexpr (TIER == TIER_BASIC) {
-        k_sincos_tab(x, s, c, ScTabLds{});
-        return;
-    }
-#endif
-    k_sincos(x, s, c);
+// ------------------------------------------------------------------ check build
+// make check (-DRT_CHECK, librt_mi355x_check.so): every ref the walk, the
+// hit record and the lights decode is checked against the count of its
+// kind's array (SceneView::n_ref); a ref past its array is counted in
+// g_check (the host's wait() turns a nonzero count into an error naming the
+// first bad ref) and read as index 0, so the run itself stays in bounds.
+// The product build compiles the check away.
+#ifdef RT_CHECK
+__device__ unsigned long long g_check[2];
+__device__ __noinline__ void check_fail(uint32_t ref) {
+    atomicAdd(&g_check[0], 1ull);
+    atomicCAS(&g_check[1], 0ull, (1ull << 32) | ref);
 }
-#ifndef RT_AB_XLOAD
-#define RT_AB_XLOAD 0
 #endif
-#if RT_AB_XLOAD
-__device__ uint32_t g_ab_sink;
+__device__ __forceinline__ uint32_t ref_idx(const SceneView& S, uint32_t ref) {
+    const uint32_t i = ref_index(ref);
+#ifdef RT_CHECK
+    const uint32_t k = ref_kind(ref);
+    if (k != K_NONE && i >= S.n_ref[k]) {
+        check_fail(ref);
+        return 0u;
+    }
 #endif
+    return i;
+}
+// a planar run's last record (DBoxF::run) must lie inside planars too
+__device__ __forceinline__ void check_run(const SceneView& S, uint32_t first, uint32_t n) {
+#ifdef RT_CHECK
+    if (n && first + n > S.n_ref[K_QUAD]) check_fail(make_ref(K_QUAD, first + n - 1));
+#endif
+}
 
 // n / d for n < 2^32, d < 2^20, from inv = 1/d rounded up: n * inv is at least
 // the quotient's integer part when d divides n (a representable product,
@@ -294,20 +285,11 @@ __device__ __forceinline__ bool sphere_t(D3 c, double radius, const Ray& r, doub
     const double disc = h * h - a * cc;
     if (disc < 0.0) return false;
     const double sq = sqrt(disc);
-#ifdef RT_AB_SPHERE_RCP
-    const double inva = 1.0 / a;  // A/B only: not the reference's rounding
-    double root = (h - sq) * inva;
-    if (!(root >= tmin && root <= tmax)) {
-        root = (h + sq) * inva;
-        if (!(root >= tmin && root <= tmax)) return false;
-    }
-#else
     double root = (h - sq) / a;
     if (!(root >= tmin && root <= tmax)) {
         root = (h + sq) / a;
         if (!(root >= tmin && root <= tmax)) return false;
     }
-#endif
     t = root;
     return true;
 }
@@ -341,18 +323,6 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
 #ifndef RT_UV_ON_DEMAND
 #define RT_UV_ON_DEMAND 1  // a planar hit's (u, v) only when its material or remap reads them
 #endif
-#ifndef RT_PLANAR_EARLY
-// 1: decide early, with the same outcome as the full test: t = num / denom
-// rounded is negative when num and denom have opposite signs (num != 0), so
-// t < tmin for tmin >= 0; with equal signs, |num| > tmax |denom| (1 + 2^-40)
-// puts the correctly rounded quotient above tmax (the product's two roundings
-// are 2^-52 apart from the margin) -- both without the f64 division; and alpha
-// out of [0, 1] rejects before beta.  Measured slower (A/B at 128 spp, min of
-// 4, r02h: C3 +4.7 %, C4 +3.6 %, C5 +2.7 %): the lanes of a wave take both
-// sides of every new branch, so no wave skips the division -- it only pays the
-// branches.  Kept as an option.
-#define RT_PLANAR_EARLY 0
-#endif
 // quad.rs:71-102 / triangle.rs:69-98 on the record's values: unit normal n,
 // parm_d D, anchor Q, edges u / v, w = n / |n|^2
 __device__ __forceinline__ bool planar_t_v(const D3 n, const double D, const D3 Q, const D3 u, const D3 v, const D3 w,
@@ -360,16 +330,10 @@ __device__ __forceinline__ bool planar_t_v(const D3 n, const double D, const D3 
     const double denom = dot(n, r.d);
     if (fabs(denom) < 1e-8) return false;
     const double num = D - dot(n, r.o);
-    if constexpr (RT_PLANAR_EARLY) {
-        const bool same = (num < 0.0) == (denom < 0.0);
-        if (!same && num != 0.0 && tmin >= 0.0) return false;
-        if (same && fabs(num) > (tmax * fabs(denom)) * (1.0 + 0x1p-40)) return false;
-    }
     const double tt = num / denom;
     if (!(tt >= tmin && tt <= tmax)) return false;
     const D3 hv = (r.o + tt * r.d) - Q;
     const double alpha = dot(w, cross(hv, v));
-    if (RT_PLANAR_EARLY && !(alpha >= 0.0 && alpha <= 1.0)) return false;
     const double beta = dot(w, cross(u, hv));
     if (!(alpha >= 0.0 && alpha <= 1.0 && beta >= 0.0 && beta <= 1.0)) return false;
     if (tri) {
@@ -667,7 +631,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
         }
         uint32_t after = REF_NONE;  // as trace_step: a primitive list element is tested in the list step
         if (ref_kind(cur) == K_LIST) {
-            const uint32_t li = ref_index(cur);
+            const uint32_t li = ref_idx(S, cur);
             const uint32_t child = S.list_children[li];
             cur = REF_NONE;
             if (child == REF_NONE) continue;
@@ -688,7 +652,7 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
                 continue;
             }
         }
-        const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+        const uint32_t kind = ref_kind(cur), idx = ref_idx(S, cur);
         cur = REF_NONE;
         double t;
         switch (kind) {
@@ -989,16 +953,8 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
     constexpr double tmin = 1e-8;
     const float tmin_f = f32_down(tmin);
     if (T.cur == REF_NONE) {
-#ifdef RT_AB_FLAT_POP
-        if (T.sp == 0) return false;
-        --T.sp;
-        const uint2 e = stk.at(T.sp);
-        if (!(__uint_as_float(e.y) <= T.cl.c_f)) return true;  // culled entry: one empty step
-        T.cur = e.x;
-#else
         T.cur = pop(stk, T.sp, 0, T.cl.c_f);
         if (T.cur == REF_NONE) return false;
-#endif
     }
     const Ray& r = FULL ? T.r : wq.get();
     uint32_t cur = T.cur;
@@ -1018,7 +974,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
     // the rest of the list pushed.
     uint32_t after = REF_NONE;
     if (ref_kind(cur) == K_LIST) {
-        const uint32_t li = ref_index(cur);
+        const uint32_t li = ref_idx(S, cur);
         const uint32_t child = S.list_children[li];
         if (child == REF_NONE) return true;  // empty list
         if constexpr (flat_runs<TIER>()) {
@@ -1027,7 +983,8 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
             // closest t so far -- what the run's single steps do
             const uint32_t ck0 = ref_kind(child);
             if (ck0 == K_QUAD || ck0 == K_TRI) {
-                const uint32_t run = S.list_boxes[li].run, n = run & 0xffu, first = ref_index(child);
+                const uint32_t run = S.list_boxes[li].run, n = run & 0xffu, first = ref_idx(S, child);
+                check_run(S, first, n);
                 RT_DIAG_ONLY(dg.sphere_tests += n;)
                 for (uint32_t k = 0; k < n; ++k) {
                     const bool tri = (run >> (8u + k)) & 1u;
@@ -1051,7 +1008,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                 // step of its own and the pop of the rest of the list
                 const bool queue = RT_FLAT_MEDIA_IN_LIST && in_box && ck == K_MEDIUM && T.nmed < RT_MEDIA_CAP;
                 if (queue) {
-                    med[T.nmed * RT_BLOCK] = make_uint4(ref_index(child), T.nxf, T.xfs.a, T.xfs.b);
+                    med[T.nmed * RT_BLOCK] = make_uint4(ref_idx(S, child), T.nxf, T.xfs.a, T.xfs.b);
                     ++T.nmed;
                 }
                 if (!in_box || queue) {
@@ -1070,7 +1027,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
             return true;
         }
     }
-    const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+    const uint32_t kind = ref_kind(cur), idx = ref_idx(S, cur);
     const uint32_t this_ref = cur;
     double t;
     bool got = false;
@@ -1085,34 +1042,21 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
         const bool planar = kind == K_TRI || kind == K_QUAD;
         // (the array addresses as values, selected: a select between the
         // SceneView's members made the compiler index a scratch copy of it)
-        const bool qn = RT_QNODES && S.qnodes != 0;
-        const uint64_t a_node = qn ? (uint64_t)S.nodes4q : (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars,
-                       a_sphere = (uint64_t)S.spheres;
+        const uint64_t a_node = (uint64_t)S.nodes4, a_planar = (uint64_t)S.planars, a_sphere = (uint64_t)S.spheres;
         uint64_t addr = a_node;
         uint32_t stride = 0u;
-        if (kind == K_BVH) stride = qn ? (uint32_t)sizeof(DNode4Q) : (uint32_t)sizeof(DNode4);
+        if (kind == K_BVH) stride = (uint32_t)sizeof(DNode4);
         if (planar) addr = a_planar, stride = (uint32_t)sizeof(DPlanar);
         if (kind == K_SPHERE) addr = a_sphere, stride = (uint32_t)sizeof(double4);
         const RT_GLOBAL float4* q = reinterpret_cast<const RT_GLOBAL float4*>(addr + (uint64_t)idx * stride);
-        // rows 0-3 hold a quantized node, a sphere (2) and half a planar
-        // record; the rest only for the lanes whose record has them
+        // rows 0-3 hold a sphere (2) and half a planar record; the rest
+        // only for the lanes whose record has them
         const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
         float4 q4 = make_float4(0.f, 0.f, 0.f, 0.f), q5 = q4, q6 = q4, q7 = q4;
-        if (planar || (kind == K_BVH && !qn)) q4 = q[4], q5 = q[5], q6 = q[6];
+        if (planar || kind == K_BVH) q4 = q[4], q5 = q[5], q6 = q[6];
         if (planar) q7 = q[7];
-#if RT_AB_XLOAD
-        {  // A/B experiment only: RT_AB_XLOAD more dwordx4 loads per walk step (the vector-memory path's cost)
-            float xs = 0.0f;
-#pragma unroll
-            for (int i = 0; i < RT_AB_XLOAD; ++i) xs += q[8 + i].x;
-            if (__float_as_uint(xs) == 0x7fc01234u) g_ab_sink = 1u;
-        }
-#endif
         if (kind == K_BVH) {
-            if (qn)
-                T.cur = visit4q_rows(q0, q1, q2, q3, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
-            else
-                T.cur = visit4_boxes_rows(q0, q1, q2, q3, q4, q5, q6, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
+            T.cur = visit4_boxes_rows(q0, q1, q2, q3, q4, q5, q6, T.rf, tmin_f, T.cl.c_f, stk, T.sp);
         } else if (kind == K_SPHERE) {
             got = sphere_t_inv(d3(f4_lo(q0), f4_hi(q0), f4_lo(q1)), f4_hi(q1), r, T.a, T.inva, tmin, T.cl.c, t);
         } else if (planar) {
@@ -1239,9 +1183,6 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #ifndef RT_SLOT_BALLOT
 #define RT_SLOT_BALLOT 1
 #endif
-#ifndef RT_SORT4
-#define RT_SORT4 1  // basic tier: the hit children sorted by entry distance before the pushes
-#endif
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
 // lane's LDS queue, pq[k * RT_BLOCK_BASIC], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
@@ -1261,7 +1202,7 @@ __device__ __forceinline__ Node4Rows load_node4(const RT_LDS float4* nl, uint32_
 }
 // visit4 on node rows already loaded
 template <class Stack>
-__device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
+__device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
                                                 float& c_f, Stack& stk, uint32_t& sp, RT_LDS uint16_t* pq, uint32_t& pn) {
     const float4 lx = nr.lx, ly = nr.ly, lz = nr.lz, hx = nr.hx, hy = nr.hy, hz = nr.hz, rq = nr.rq;
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
@@ -1281,7 +1222,7 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
     for (int i = 0; i < 4; ++i) {
         if (__ballot(sph[i])) {
             if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
-                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_index(R[i]);
+                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_idx(S, R[i]);
                 ++pn;
             }
         }
@@ -1303,7 +1244,7 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
-                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_index(R[i]);
+                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_idx(S, R[i]);
                 ++pn;
             }
         }
@@ -1317,7 +1258,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
         ref[i] = R[i];
     }
 #endif
-#if RT_SORT4
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];
@@ -1336,23 +1276,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const Node4Rows& nr, const RayF&
     if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
     if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
     return key[0] < INF ? ref[0] : REF_NONE;
-#else
-    // the nearest hit child is walked next; the others are pushed in slot
-    // order, unsorted (A/B option)
-    float bk = key[0];
-    uint32_t bi = 0;
-#pragma unroll
-    for (int i = 1; i < 4; ++i) {
-        const bool lt = key[i] < bk;
-        bk = lt ? key[i] : bk;
-        bi = lt ? (uint32_t)i : bi;
-    }
-#pragma unroll
-    for (int i = 3; i >= 0; --i)
-        if ((uint32_t)i != bi && key[i] < INF) stk.push(sp++, ref[i], key[i]);
-    const uint32_t br = bi == 0 ? ref[0] : bi == 1 ? ref[1] : bi == 2 ? ref[2] : ref[3];
-    return bk < INF ? br : REF_NONE;
-#endif
 }
 
 // One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
@@ -1374,37 +1297,9 @@ __device__ __forceinline__ uint32_t visit4_boxes_rows(const float4 lx, const flo
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
     return visit4_core(LX, LY, LZ, HX, HY, HZ, R, rf, tmin_f, c_f, stk, sp);
 }
-// A DNode4Q's four rows (rt_layout.h): the children's boxes decoded as
-// fmaf(q, scale, origin) (rt_qnode.h) -- boxes that contain the f32 boxes
-// the 112-B node stores -- then the same visit.
-template <class Stack>
-__device__ __forceinline__ uint32_t visit4q_rows(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
-                                                 const RayF& rf, float tmin_f, float c_f, Stack& stk, uint32_t& sp) {
-    const uint32_t ex = __float_as_uint(r0.w);
-    const float sx = __uint_as_float((ex & 0xffu) << 23), sy = __uint_as_float(((ex >> 8) & 0xffu) << 23),
-                sz = __uint_as_float(((ex >> 16) & 0xffu) << 23);
-    const uint32_t qlx = __float_as_uint(r1.x), qly = __float_as_uint(r1.y), qlz = __float_as_uint(r1.z);
-    const uint32_t qhx = __float_as_uint(r1.w), qhy = __float_as_uint(r2.x), qhz = __float_as_uint(r2.y);
-    float LX[4], LY[4], LZ[4], HX[4], HY[4], HZ[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        LX[i] = qnode_decode(r0.x, sx, (qlx >> (8 * i)) & 0xffu);
-        LY[i] = qnode_decode(r0.y, sy, (qly >> (8 * i)) & 0xffu);
-        LZ[i] = qnode_decode(r0.z, sz, (qlz >> (8 * i)) & 0xffu);
-        HX[i] = qnode_decode(r0.x, sx, (qhx >> (8 * i)) & 0xffu);
-        HY[i] = qnode_decode(r0.y, sy, (qhy >> (8 * i)) & 0xffu);
-        HZ[i] = qnode_decode(r0.z, sz, (qhz >> (8 * i)) & 0xffu);
-    }
-    const uint32_t R[4] = {__float_as_uint(r3.x), __float_as_uint(r3.y), __float_as_uint(r3.z), __float_as_uint(r3.w)};
-    return visit4_core(LX, LY, LZ, HX, HY, HZ, R, rf, tmin_f, c_f, stk, sp);
-}
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_boxes(const SceneView& S, uint32_t idx, const RayF& rf, float tmin_f,
                                                  float c_f, Stack& stk, uint32_t& sp) {
-    if (RT_QNODES && S.qnodes) {
-        const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4q + idx);
-        return visit4q_rows(np[0], np[1], np[2], np[3], rf, tmin_f, c_f, stk, sp);
-    }
     const RT_GLOBAL float4* np = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4 + idx);
     return visit4_boxes_rows(np[0], np[1], np[2], np[3], np[4], np[5], np[6], rf, tmin_f, c_f, stk, sp);
 }
@@ -1497,7 +1392,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
         cur = T.cur;
         T.cur = REF_NONE;
     }
-    const uint32_t kind = ref_kind(cur), idx = ref_index(cur);
+    const uint32_t kind = ref_kind(cur), idx = ref_idx(S, cur);
     const Node4Rows rows = load_node4(nl, kind == K_BVH ? idx : 0u);
     if (round) {  // sphere round (sphere.rs:77-108)
         RT_DIAG_ONLY(++dg.sphere_tests;)
@@ -1525,7 +1420,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     }
     if (kind == K_BVH) {
         RT_DIAG_ONLY(++dg.node_visits;)
-        T.cur = visit4_rows(rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
+        T.cur = visit4_rows(S, rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
     }
     T.pn = pn;
     return T.cur != REF_NONE || T.sp > 0 || pn > 0;
@@ -1547,7 +1442,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     Ray r = wr;
     if constexpr (FULL)
         for (uint32_t k = 0; k < h.nxf; ++k) r = xf_ray(S.xforms[h.xf.get(k)], r);
-    const uint32_t kind = ref_kind(h.ref), idx = ref_index(h.ref);
+    const uint32_t kind = ref_kind(h.ref), idx = ref_idx(S, h.ref);
     Rec rec;
     rec.u = 0.0;
     rec.v = 0.0;
@@ -1644,7 +1539,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
 
 // ------------------------------------------------------------------ lights (pdf.rs:66-88)
 __device__ double light_pdf_one(const SceneView& S, uint32_t ref, D3 o, D3 d) {
-    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    const uint32_t kind = ref_kind(ref), idx = ref_idx(S, ref);
     const Ray r{o, d, 0.0};
     double t;
     if (kind == K_QUAD || kind == K_TRI) {  // quad.rs:108-120
@@ -1671,7 +1566,7 @@ __device__ double light_pdf(const SceneView& S, D3 o, D3 d) {
     if (ref_kind(root) != K_LIST) return light_pdf_one(S, root, o, d);
     double sum = 0.0;  // hits.rs:52-67
     uint32_t n = 0;
-    for (uint32_t i = ref_index(root); S.list_children[i] != REF_NONE; ++i, ++n) sum += light_pdf_one(S, S.list_children[i], o, d);
+    for (uint32_t i = ref_idx(S, root); S.list_children[i] != REF_NONE; ++i, ++n) sum += light_pdf_one(S, S.list_children[i], o, d);
     return sum / (double)n;
 }
 __device__ __forceinline__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21, 34-38
@@ -1683,7 +1578,7 @@ __device__ __forceinline__ D3 onb_world(D3 n, D3 v, bool& ok) {  // onb.rs:8-21,
 // Quad / Triangle / Sphere::random (quad.rs:122-125, triangle.rs:117-128, sphere.rs:134-144)
 __device__ __forceinline__ D3 light_random_one(const SceneView& S, uint32_t ref, D3 o, Rng& rng, uint32_t& ovf,
                                                bool& ok) {
-    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    const uint32_t kind = ref_kind(ref), idx = ref_idx(S, ref);
     if (kind == K_QUAD || kind == K_TRI) {  // quad.rs:122-125, triangle.rs:117-128
         const DPlanar& P = S.planars[idx];
         double a = rng.next(ovf);
@@ -1718,7 +1613,7 @@ __device__ D3 light_random(const SceneView& S, D3 o, Rng& rng, uint32_t& ovf, bo
     uint32_t ref = S.lights_root;
     if (ref_kind(ref) == K_LIST) {  // hits.rs:69-75 choose
         uint32_t n = 0;
-        for (uint32_t i = ref_index(ref); S.list_children[i] != REF_NONE; ++i) ++n;
+        for (uint32_t i = ref_idx(S, ref); S.list_children[i] != REF_NONE; ++i) ++n;
         uint32_t k = (uint32_t)(rng.next(ovf) * (double)n);
         if (k >= n) k = n - 1;
         ref = S.list_children[ref_index(ref) + k];
@@ -1739,7 +1634,7 @@ constexpr int RT_LIGHT_DEPTH = 4;  // list / Transform levels of a lights tree (
 
 __device__ double light_pdf_leaf(const SceneView& S, uint32_t ref, D3 o, D3 d) {
     if (ref_kind(ref) != K_MSPHERE) return light_pdf_one(S, ref, o, d);
-    const double4 s = S.msph_center[ref_index(ref)];  // Ray::new: time 0 (ray.rs:11-17) -> center.at(0)
+    const double4 s = S.msph_center[ref_idx(S, ref)];  // Ray::new: time 0 (ray.rs:11-17) -> center.at(0)
     const Ray r{o, d, 0.0};
     double t;
     if (!sphere_t(d3(s.x, s.y, s.z), s.w, r, len2(d), 1e-8, __builtin_huge_val(), t)) return 0.0;
@@ -1751,7 +1646,7 @@ __device__ double light_pdf_leaf(const SceneView& S, uint32_t ref, D3 o, D3 d) {
 
 template <int D>
 __device__ double light_pdf_tree(const SceneView& S, uint32_t ref, D3 o, D3 d, bool& panic) {
-    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    const uint32_t kind = ref_kind(ref), idx = ref_idx(S, ref);
     if constexpr (D > 0) {
         if (kind == K_LIST) {  // hits.rs:52-67
             double sum = 0.0;
@@ -1774,7 +1669,7 @@ __device__ double light_pdf_tree(const SceneView& S, uint32_t ref, D3 o, D3 d, b
 
 template <int D>
 __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng, uint32_t& ovf, bool& ok) {
-    const uint32_t kind = ref_kind(ref), idx = ref_index(ref);
+    const uint32_t kind = ref_kind(ref), idx = ref_idx(S, ref);
     if constexpr (D > 0) {
         if (kind == K_LIST) {  // hits.rs:69-75 choose
             uint32_t n = 0;
@@ -1904,7 +1799,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     if constexpr (HOIST) {
         xi0 = rng.next(ovf);
         xi1 = rng.next(ovf);
-        t_sincos<TIER>(2.0 * PI * xi0, &sn0, &cs0);
+        k_sincos(2.0 * PI * xi0, &sn0, &cs0);
     }
     if constexpr (TIER == TIER_FULL_GL) {
         if (M.flags & MF_EMISSIVE) L = L + beta * emitted_tree<RT_MAT_DEPTH>(S, rec.mat, rec.u, rec.v, rec.p);
@@ -2182,9 +2077,6 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         const uint32_t n_lds = min(S.n_nodes4, NODE_LDS_CAP);  // == n_nodes4 (launcher)
         const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
         for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) node_lds[k] = src[k];
-#if RT_SC_LDS
-        for (uint32_t k = threadIdx.x; k < 256u * 4u; k += BLK) g_sc_lds[k] = (&RTCR_SC_PIO128[0][0])[k];
-#endif
         __syncthreads();
     }
     if constexpr (tier_full_bvh(TIER) && RT_PERLIN_LDS) {
@@ -2329,7 +2221,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
                 const double rr = sqrt(rng.next(ovf));
                 double sn, cs;
-                t_sincos<TIER>(theta, &sn, &cs);
+                k_sincos(theta, &sn, &cs);
                 origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
             }
             ray.o = origin;
@@ -2537,6 +2429,18 @@ extern "C" int rt_lane_trace(unsigned long long* out, uint64_t n_lanes) {
                                     n_lanes * rtk::RT_TRACE_W * sizeof(unsigned long long));
 }
 #endif
+#if defined(RT_CHECK)
+// check build: {refs past their arrays, 1 << 32 | the first bad ref} on the
+// current device (rt_render.cpp wait())
+extern "C" int rtk_check_read(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_check), sizeof(unsigned long long) * 2);
+    if (reset) {
+        unsigned long long z[2] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_check), z, sizeof z);
+    }
+    return (int)e;
+}
+#endif
 #if defined(RT_DIAG)
 // diagnostic build: the counters live with the (DIAG_TIER) kernel that adds to them
 extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
@@ -2691,7 +2595,6 @@ extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
 }
 
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
-extern "C" int rtk_qnodes(void) { return RT_QNODES; }
 extern "C" int rtk_planar_filter(void) { return RT_PLANAR_FILTER; }
 extern "C" int rtk_block_threads(int tier) { return tier == rtk::TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK; }
 extern "C" int rtk_mesh_bvh4(void) { return RT_MESH_BVH4; }

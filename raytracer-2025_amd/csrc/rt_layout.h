@@ -89,26 +89,6 @@ struct alignas(16) DNode4 {
 };
 static_assert(sizeof(DNode4) == 112, "DNode4 must be 112 B (7 dwordx4)");
 
-// Mesh / full-tier 4-wide node in 64 B (4 dwordx4 instead of DNode4's 7):
-// each child's box quantized to 8 bits per bound in the frame of the node's
-// own box -- origin = the union's f32 lower corner, per-axis scale 2^(e - 127)
-// -- and decoded as fmaf(q, scale, origin), one rounding.  The encoder
-// (rt_qnode.h) picks each lower bound's q as the largest whose decoded value
-// is <= the child's f32 lower bound and each upper bound's as the smallest
-// whose decoded value is >= its upper bound, so the decoded box contains the
-// child's box and rt_slab.h's conservative test applies to it unchanged
-// (tests/test_qnode_cpu.py).  Rows: {origin, exps} {qlo x y z, qhi x}
-// {qhi y z, 0, 0} {refs}; an empty slot has qlo = 255, qhi = 0 and REF_NONE.
-struct alignas(16) DNode4Q {
-    float origin[3];
-    uint32_t exps;     // byte a: biased f32 exponent of axis a's scale
-    uint32_t qlo[3];   // axis a: byte i = child i's lower bound
-    uint32_t qhi[3];   // axis a: byte i = child i's upper bound
-    uint32_t pad[2];
-    uint32_t ref[4];
-};
-static_assert(sizeof(DNode4Q) == 64, "DNode4Q must be 64 B (4 dwordx4)");
-
 // f32 box of one list element (list_boxes, parallel to list_children),
 // rounded outward: the flat tier tests it before the element itself.  run:
 // for a quad / triangle element, the number n (<= RT_PLANAR_RUN_MAX) of
@@ -228,8 +208,7 @@ struct alignas(16) DPerlin {
 // Everything the kernel reads about the world, as device pointers.
 struct SceneView {
     const RT_GLOBAL DNode* nodes;
-    const RT_GLOBAL DNode4* nodes4;          // basic tier (and mesh / full tiers without qnodes): K_BVH refs index these
-    const RT_GLOBAL DNode4Q* nodes4q;        // mesh / full tiers with qnodes: K_BVH refs index these
+    const RT_GLOBAL DNode4* nodes4;          // 4-wide nodes: K_BVH refs index these
     const RT_GLOBAL double4* spheres;        // {cx, cy, cz, r}
     const RT_GLOBAL int32_t* sphere_mat;
     const RT_GLOBAL double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}
@@ -257,7 +236,10 @@ struct SceneView {
     uint32_t features;       // F_* of everything reachable from world/lights
     uint32_t n_nodes4;       // entries of nodes4
     uint32_t n_perlin;       // entries of perlin (the full tiers copy the first into LDS)
-    uint32_t qnodes;         // mesh / full tiers: the BVH nodes are DNode4Q (nodes4q)
+    // records each ref kind indexes (K_BVH: nodes4 or the two-box nodes,
+    // K_LIST: list_children, K_QUAD / K_TRI: planars, ...): the check build
+    // (make check, -DRT_CHECK) verifies every decoded ref against it
+    uint32_t n_ref[16];
 };
 
 // Scene features; the launcher picks the smallest kernel tier covering them.

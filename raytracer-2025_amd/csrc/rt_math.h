@@ -64,14 +64,6 @@ __device__ __forceinline__ void k_sincos(double x, double* s, double* c) {
     else
         ::sincos(x, s, c);
 }
-// The same with the sin / cos (k pi/128) records read through `tab` (an LDS copy).
-template <class Tab>
-__device__ __forceinline__ void k_sincos_tab(double x, double* s, double* c, const Tab& tab) {
-    if (RT_CRMATH)
-        rtcr::sincos_tab(x, s, c, tab);
-    else
-        ::sincos(x, s, c);
-}
 
 // ---------------------------------------------------------------- RNG
 __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,

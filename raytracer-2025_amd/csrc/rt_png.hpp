@@ -42,7 +42,7 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
     static const uint8_t SIG[8] = {137, 80, 78, 71, 13, 10, 26, 10};
     if (f.size() < 8 || std::memcmp(f.data(), SIG, 8) != 0) {
         err = "not a PNG file";
-        return UNSUPPORTED;
+        return CORRUPT;
     }
     size_t pos = 8;
     int depth = 0, ctype = -1, interlace = 0;
@@ -96,8 +96,8 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
         return CORRUPT;
     }
     if ((uint64_t)W * H > (1ull << 28)) {
-        err = "PNG too large";
-        return UNSUPPORTED;
+        err = "PNG larger than this library's 2^28-pixel limit";
+        return UNSUPPORTED;  // a library limit, not a bad file
     }
     const size_t bpp_bits = (size_t)channels * depth;
     const size_t bpp = std::max<size_t>(1, bpp_bits / 8);  // filter byte distance

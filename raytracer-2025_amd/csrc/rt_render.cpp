@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <map>
 #include <thread>
@@ -80,6 +81,11 @@ RcclApi& rccl() {
 struct rt_comm {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0, device = -1;
+    // held from ncclGroupStart to ncclGroupEnd: two scenes gathering through
+    // one communicator from two threads enqueue their groups one after the
+    // other, never interleaved (RCCL matches a communicator's sends and
+    // receives in enqueue order)
+    std::mutex group;
 };
 
 namespace rth {
@@ -144,7 +150,7 @@ struct RenderState {
     bool g_recorded = false;
     // ncclCommInitAll communicators of the last device list with distinct devices
     std::vector<int> comm_devices;
-    std::vector<ncclComm_t> comms;
+    std::shared_ptr<struct CommSet> comm_set;
     // the last render
     int n_parts = 0;
     bool gathered = false;
@@ -193,10 +199,20 @@ static void free_root_buffers(RenderState* r) {
 // ncclCommInitAll communicators are process-wide, one set per device list,
 // shared by every scene that renders on that list and kept until the process
 // exits: building a set is slow, and scenes (or calls) that alternate device
-// lists would otherwise rebuild them each time.
+// lists would otherwise rebuild them each time.  A set is used by one gather
+// at a time: the gather holds the set's `group` lock from ncclGroupStart to
+// ncclGroupEnd, so that scenes rendering on the same device list from
+// different threads (rt_mi355x.h: different scenes may be used from
+// different threads) enqueue whole groups one after the other -- RCCL matches
+// a communicator's sends and receives in enqueue order, and interleaved
+// groups could hang or swap two scenes' rows.
+struct CommSet {
+    std::mutex group;
+    std::vector<ncclComm_t> comms;
+};
 struct CommCache {
-    std::mutex m;
-    std::map<std::vector<int>, std::vector<ncclComm_t>> sets;
+    std::mutex m;  // the map only
+    std::map<std::vector<int>, std::shared_ptr<CommSet>> sets;
 };
 static CommCache& comm_cache() {
     static CommCache* c = new CommCache();  // never destroyed: RCCL may already be torn down at exit
@@ -204,22 +220,23 @@ static CommCache& comm_cache() {
 }
 static int32_t nccl_fail(ncclResult_t e, const char* what);
 static int32_t acquire_comms(RenderState* r, const std::vector<int>& devs) {
-    if (r->comm_devices == devs && !r->comms.empty()) return RT_OK;
+    if (r->comm_devices == devs && r->comm_set) return RT_OK;
     CommCache& cc = comm_cache();
     std::lock_guard<std::mutex> lk(cc.m);
     auto it = cc.sets.find(devs);
     if (it == cc.sets.end()) {
-        std::vector<ncclComm_t> comms(devs.size(), nullptr);
-        const ncclResult_t ne = rccl().comm_init_all(comms.data(), (int)devs.size(), devs.data());
+        auto set = std::make_shared<CommSet>();
+        set->comms.assign(devs.size(), nullptr);
+        const ncclResult_t ne = rccl().comm_init_all(set->comms.data(), (int)devs.size(), devs.data());
         if (ne != ncclSuccess) return nccl_fail(ne, "ncclCommInitAll");
-        it = cc.sets.emplace(devs, std::move(comms)).first;
+        it = cc.sets.emplace(devs, std::move(set)).first;
     }
-    r->comms = it->second;
+    r->comm_set = it->second;
     r->comm_devices = devs;
     return RT_OK;
 }
 static void destroy_comms(RenderState* r) {  // the scene lets go of its cached set
-    r->comms.clear();
+    r->comm_set.reset();
     r->comm_devices.clear();
 }
 
@@ -258,20 +275,6 @@ static int prepare_tier(HostWorld& hw) {
                                      std::to_string(RT_STACK_MAX));
             return -1;
         }
-    }
-    // mesh / full tiers walk their nodes from global memory: lay them (and
-    // the primitives they name) out for the walk (rth::bvh4_relayout);
-    // RT_BVH4_LAYOUT=<mode> in the environment overrides the default (A/B)
-    if (tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
-        const char* l = std::getenv("RT_BVH4_LAYOUT");
-        bvh4_relayout(hw, l && l[0] ? std::atoi(l) : RT_BVH4_LAYOUT);
-    }
-    // mesh / full tiers of a kernel built with RT_QNODES: 64-B quantized nodes
-    // (rt_qnode.h) unless a bound is not finite (then the 112-B f32 nodes);
-    // RT_QNODES=0 in the environment keeps f32 nodes (A/B)
-    if (rtk_qnodes() && tier != rtk::TIER_BASIC && tier != rtk::TIER_FULL_FLAT && !hw.nodes4.empty()) {
-        const char* q = std::getenv("RT_QNODES");
-        if (!(q && q[0] == '0')) bvh4_quantize(hw);
     }
     return tier;
 }
@@ -315,6 +318,21 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     int32_t rc = flatten(s, world, lights, bg, reference_bvh, hw);
     int tier = rc == RT_OK ? prepare_tier(hw) : -1;
     if (rc == RT_OK && tier < 0) rc = RT_ESTACK;
+#ifdef RT_CHECK
+    // check build only: RT_CHECK_INJECT=1 makes every node slot that names a
+    // primitive name a record past its array -- the kind of fault the check
+    // is for (a bad relayout once did this silently); tests/test_check_gpu.py
+    // expects the render to report it
+    if (rc == RT_OK && std::getenv("RT_CHECK_INJECT") && std::getenv("RT_CHECK_INJECT")[0] == '1') {
+        for (rtk::DNode4& nd : hw.nodes4)
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t kind = rtk::ref_kind(nd.ref[k]);
+                const size_t n = kind == rtk::K_SPHERE ? hw.spheres.size()
+                                 : (kind == rtk::K_QUAD || kind == rtk::K_TRI) ? hw.planars.size() : 0;
+                if (n) nd.ref[k] = rtk::make_ref(kind, (uint32_t)n + rtk::ref_index(nd.ref[k]));
+            }
+    }
+#endif
     if (rc == RT_OK) {
         const uint32_t stack_cap = rtk_stack_entries(tier);
         if (hw.stack_need > stack_cap)
@@ -331,7 +349,6 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     rtk::SceneView& v = fw.rel;
     v.nodes = (const rtk::DNode*)off(put(blob, hw.nodes));
     v.nodes4 = (const rtk::DNode4*)off(put(blob, hw.nodes4));
-    v.nodes4q = (const rtk::DNode4Q*)off(put(blob, hw.nodes4q));
     v.spheres = (const double4*)off(put(blob, hw.spheres));
     v.sphere_mat = (const int32_t*)off(put(blob, hw.sphere_mat));
     v.msph_center = (const double4*)off(put(blob, hw.msph_center));
@@ -362,8 +379,16 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.stack_need = hw.stack_need;
     v.features = hw.features;
     v.n_nodes4 = (uint32_t)hw.nodes4.size();
-    v.qnodes = hw.qnodes ? 1u : 0u;
     v.n_perlin = (uint32_t)hw.perlin.size();
+    std::memset(v.n_ref, 0, sizeof v.n_ref);
+    v.n_ref[rtk::K_BVH] = (uint32_t)std::max(hw.nodes4.size(), hw.nodes.size());
+    v.n_ref[rtk::K_LIST] = (uint32_t)hw.list_children.size();
+    v.n_ref[rtk::K_SPHERE] = (uint32_t)hw.spheres.size();
+    v.n_ref[rtk::K_MSPHERE] = (uint32_t)hw.msph_center.size();
+    v.n_ref[rtk::K_QUAD] = v.n_ref[rtk::K_TRI] = (uint32_t)hw.planars.size();
+    v.n_ref[rtk::K_XFORM] = (uint32_t)hw.xforms.size();
+    v.n_ref[rtk::K_MEDIUM] = (uint32_t)hw.media.size();
+    v.n_ref[rtk::K_POPXF] = 1;  // the marker's index is 0
     fw.tier = tier;
     fw.stack_need = hw.stack_need;
     fw.n_prims = hw.n_prims;
@@ -446,7 +471,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     char* b = d->blob;
     rtk::SceneView v = fw.rel;
     auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
-    fix(v.nodes), fix(v.nodes4), fix(v.nodes4q), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
+    fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
         fix(v.msph_mat), fix(v.planars), fix(v.planars_f), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
         fix(v.remap_nm), fix(v.list_children), fix(v.list_boxes), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
         fix(v.texels), fix(v.perlin);
@@ -816,6 +841,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
             for (uint32_t j = i + 1; j < nd; ++j) distinct = distinct && opts->devices[i] != opts->devices[j];
         if (comm) {
             if (!nc.ok) return abort_render(set_error(RT_EDEVICE, nc.err));
+            std::lock_guard<std::mutex> glk(comm->group);  // the whole group, enqueued at once
             ncclResult_t ne = nc.group_start();
             if (ne == ncclSuccess)
                 ne = nc.send(root.out_used, (size_t)root.rows * row_floats, ncclFloat32, 0, comm->comm, rs);
@@ -834,20 +860,22 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         } else if (distinct && nc.ok) {
             const std::vector<int> devs(opts->devices, opts->devices + nd);
             if ((rc = acquire_comms(r, devs)) != RT_OK) return abort_render(rc);
+            CommSet& cs = *r->comm_set;
+            std::lock_guard<std::mutex> glk(cs.group);  // the whole group, enqueued at once
             ncclResult_t ne = nc.group_start();
             for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
-                ne = nc.send(parts[k].out_used, (size_t)parts[k].rows * row_floats, ncclFloat32, 0, r->comms[k],
+                ne = nc.send(parts[k].out_used, (size_t)parts[k].rows * row_floats, ncclFloat32, 0, cs.comms[k],
                              parts[k].stream);
                 if (ne == ncclSuccess && want_srgb)
-                    ne = nc.send(parts[k].d->srgb, (size_t)parts[k].rows * row_floats, ncclUint8, 0, r->comms[k],
+                    ne = nc.send(parts[k].d->srgb, (size_t)parts[k].rows * row_floats, ncclUint8, 0, cs.comms[k],
                                  parts[k].stream);
             }
             for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
                 ne = nc.recv(r->staging + k * slice, (size_t)parts[k].rows * row_floats, ncclFloat32, (int)k,
-                             r->comms[0], rs);
+                             cs.comms[0], rs);
                 if (ne == ncclSuccess && want_srgb)
                     ne = nc.recv(r->staging_srgb + k * slice, (size_t)parts[k].rows * row_floats, ncclUint8, (int)k,
-                                 r->comms[0], rs);
+                                 cs.comms[0], rs);
             }
             const ncclResult_t ge = nc.group_end();
             if (ne != ncclSuccess) return abort_render(nccl_fail(ne, "ncclSend/ncclRecv"));
@@ -885,6 +913,11 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     return RT_OK;
 }
 
+// check build only (make check): the kernel's count of decoded refs past
+// their arrays on the current device (rt_kernel.hip ref_idx); absent from
+// the product library
+extern "C" __attribute__((weak)) int rtk_check_read(unsigned long long* out, int reset);
+
 static int32_t wait(rt_scene* s, rt_stats* st) {
     RenderState* r = s ? s->rs : nullptr;
     if (st) std::memset(st, 0, sizeof(*st));
@@ -901,6 +934,18 @@ static int32_t wait(rt_scene* s, rt_stats* st) {
         if ((e = hipMemcpy(h, d->stats, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) return hip_fail(e, "stats copy");
         rays += h[0];
         panics += h[1];
+        if (rtk_check_read) {
+            unsigned long long c[2] = {0, 0};
+            if ((e = (hipError_t)rtk_check_read(c, 1)) != hipSuccess) return hip_fail(e, "check counters");
+            if (c[0]) {
+                const uint32_t bad = (uint32_t)c[1];
+                r->pending = false;
+                return set_error(RT_EPANIC, "check build: " + std::to_string(c[0]) +
+                                                " decoded ref(s) past their array (first: kind " +
+                                                std::to_string(rtk::ref_kind(bad)) + ", index " +
+                                                std::to_string(rtk::ref_index(bad)) + ")");
+            }
+        }
         samples += d->samples;
         float ms = 0;
         if (d->ran) (void)hipEventElapsedTime(&ms, d->ev_start, d->ev_stop);
@@ -965,7 +1010,6 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
         const int tier = prepare_tier(hw);
         if (tier < 0) return RT_ESTACK;
         if (!hw.nodes4.empty()) out->bvh_nodes = (uint32_t)hw.nodes4.size();
-        if (hw.qnodes) out->bvh_nodes = (uint32_t)hw.nodes4q.size();
         out->stack_need = hw.stack_need;
         out->kernel_tier = (uint32_t)tier;
         out->features = hw.features;

@@ -2,7 +2,6 @@
 // world flattener.  Host code only; the device half is rt_render.hip.
 #include "rt_kernel.h"
 #include "rt_image.hpp"
-#include "rt_qnode.h"
 #include "rt_scene.hpp"
 
 #include <algorithm>
@@ -1676,113 +1675,4 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
     return sn;
 }
 
-void bvh4_relayout(HostWorld& hw, int mode) {
-    using rtk::REF_NONE;
-    if (mode <= 0 || hw.nodes4.empty()) return;
-    const size_t n = hw.nodes4.size();
-    // new position of each node: a node's inner children get consecutive
-    // slots (so the siblings a walk pops are neighbours), depth first
-    constexpr uint32_t UNSET = UINT32_MAX;  // (REF_NONE is 0: a valid position)
-    std::vector<uint32_t> at(n, UNSET), order;
-    order.reserve(n);
-    std::vector<uint32_t> todo;
-    auto place = [&](uint32_t ref) {
-        if (rtk::ref_kind(ref) != rtk::K_BVH) return false;
-        const uint32_t i = rtk::ref_index(ref);
-        if (i >= n || at[i] != UNSET) return false;
-        at[i] = (uint32_t)order.size();
-        order.push_back(i);
-        return true;
-    };
-    auto lay = [&](uint32_t root) {
-        if (!place(root)) return;
-        todo.push_back(rtk::ref_index(root));
-        while (!todo.empty()) {
-            const uint32_t i = todo.back();
-            todo.pop_back();
-            uint32_t placed[4], np = 0;
-            for (int s = 0; s < 4; ++s)
-                if (place(hw.nodes4[i].ref[s])) placed[np++] = rtk::ref_index(hw.nodes4[i].ref[s]);
-            while (np) todo.push_back(placed[--np]);  // the first child's subtree next
-        }
-    };
-    lay(hw.world_root);
-    for (uint32_t r : hw.list_children) lay(r);
-    for (const rtk::DXform& x : hw.xforms) lay(x.child);
-    for (const rtk::DMedium& m : hw.media) lay(m.boundary);
-    if (order.size() != n) return;  // a node no root reaches: keep the build order
-    auto remap = [&](uint32_t r) {
-        return rtk::ref_kind(r) == rtk::K_BVH ? rtk::make_ref(rtk::K_BVH, at[rtk::ref_index(r)]) : r;
-    };
-    std::vector<rtk::DNode4> nodes(n);
-    for (size_t k = 0; k < n; ++k) {
-        nodes[k] = hw.nodes4[order[k]];
-        for (int s = 0; s < 4; ++s) nodes[k].ref[s] = remap(nodes[k].ref[s]);
-    }
-    hw.nodes4 = std::move(nodes);
-    hw.world_root = remap(hw.world_root);
-    for (uint32_t& r : hw.list_children) r = remap(r);
-    for (rtk::DXform& x : hw.xforms) x.child = remap(x.child);
-    for (rtk::DMedium& m : hw.media) m.boundary = remap(m.boundary);
-    // mode 2: the quad / triangle records in the order the nodes name them,
-    // so a leaf node's primitives share lines.  Media name their boundary
-    // quads as a range (DMedium::planar_first): worlds with media keep theirs.
-    if (mode < 2 || !hw.media.empty() || hw.planars.empty()) return;
-    const size_t np = hw.planars.size();
-    std::vector<uint32_t> pat(np, UNSET), porder;
-    porder.reserve(np);
-    auto pplace = [&](uint32_t r) {
-        const uint32_t k = rtk::ref_kind(r);
-        if (k != rtk::K_QUAD && k != rtk::K_TRI) return;
-        const uint32_t i = rtk::ref_index(r);
-        if (i < np && pat[i] == UNSET) {
-            pat[i] = (uint32_t)porder.size();
-            porder.push_back(i);
-        }
-    };
-    for (const rtk::DNode4& nd : hw.nodes4)
-        for (int s = 0; s < 4; ++s) pplace(nd.ref[s]);
-    for (uint32_t i = 0; i < np; ++i)
-        if (pat[i] == UNSET) {
-            pat[i] = (uint32_t)porder.size();
-            porder.push_back(i);
-        }
-    auto permute = [&](auto& v) {
-        if (v.size() != np) return;
-        auto old = v;
-        for (size_t k = 0; k < np; ++k) v[k] = old[porder[k]];
-    };
-    permute(hw.planars);
-    permute(hw.planars_f);
-    permute(hw.planar_area);
-    permute(hw.planar_mat);
-    permute(hw.planar_remap);
-    auto premap = [&](uint32_t r) {
-        const uint32_t k = rtk::ref_kind(r);
-        return (k == rtk::K_QUAD || k == rtk::K_TRI) ? rtk::make_ref(k, pat[rtk::ref_index(r)]) : r;
-    };
-    for (rtk::DNode4& nd : hw.nodes4)
-        for (int s = 0; s < 4; ++s) nd.ref[s] = premap(nd.ref[s]);
-    hw.world_root = premap(hw.world_root);
-    hw.lights_root = premap(hw.lights_root);
-    for (uint32_t& r : hw.list_children) r = premap(r);
-    for (rtk::DXform& x : hw.xforms) x.child = premap(x.child);
-}
-
-bool bvh4_quantize(HostWorld& hw) {
-    std::vector<rtk::DNode4Q> q(hw.nodes4.size());
-    for (size_t k = 0; k < hw.nodes4.size(); ++k) {
-        QNode e;
-        if (!qnode_encode(hw.nodes4[k].lo, hw.nodes4[k].hi, hw.nodes4[k].ref, e)) return false;
-        rtk::DNode4Q& n = q[k];
-        n = rtk::DNode4Q{};
-        for (int a = 0; a < 3; ++a) n.origin[a] = e.origin[a], n.qlo[a] = e.qlo[a], n.qhi[a] = e.qhi[a];
-        n.exps = e.exps;
-        for (int i = 0; i < 4; ++i) n.ref[i] = hw.nodes4[k].ref[i];
-    }
-    hw.nodes4q = std::move(q);
-    hw.nodes4.clear();
-    hw.qnodes = true;
-    return true;
-}
 }  // namespace rth

@@ -108,8 +108,6 @@ struct MatRec {
 struct HostWorld {
     std::vector<rtk::DNode> nodes;
     std::vector<rtk::DNode4> nodes4;  // basic tier (bvh4_basic); mesh / full tiers before bvh4_quantize
-    std::vector<rtk::DNode4Q> nodes4q;  // mesh / full tiers: quantized nodes (qnodes)
-    bool qnodes = false;
     std::vector<double4> spheres;
     std::vector<int32_t> sphere_mat;
     std::vector<double4> msph_center, msph_dir;
@@ -165,19 +163,5 @@ int32_t flatten(const rt_scene* s, int32_t world, int32_t lights, int32_t backgr
 // unchanged when it exceeds max_need), or UINT32_MAX (hw unchanged) when the
 // tree would have more than max_nodes nodes.
 uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, size_t max_nodes = SIZE_MAX);
-// Re-lays out the 4-wide nodes of a converted world (same topology, refs
-// rewritten): mode 0 keeps the build's depth-first order; 1 places a node's
-// inner children consecutively (depth first over the sibling groups); 2
-// also stores the quad / triangle records in the order the nodes name them
-// (worlds without media).  Measured without effect: an
-// A/B option, default 0.
-#ifndef RT_BVH4_LAYOUT
-#define RT_BVH4_LAYOUT 0
-#endif
-void bvh4_relayout(HostWorld& hw, int mode);
-// Mesh / full tiers: re-encodes hw.nodes4 (boxed children only) as 64-B
-// quantized nodes (hw.nodes4q, rt_qnode.h) and sets hw.qnodes; false (hw
-// unchanged) when a node's bounds are not finite or span more than 2^100.
-bool bvh4_quantize(HostWorld& hw);
 void destroy_render_state(RenderState* r);
 }  // namespace rth

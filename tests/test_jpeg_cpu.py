@@ -33,12 +33,17 @@ REF_JPEG = "/root/reference/assets/Final/normal.jpg"
 PIL = pytest.importorskip("PIL.Image")
 
 
-@pytest.fixture(scope="module")
-def load():
+def _harness(sanitize):
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "img_dump.%d" % os.getpid())
-    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", os.path.join(HERE, "cpp", "img_dump.cpp"), "-o",
+    exe = os.path.join(BUILD, "img_dump%s.%d" % ("_asan" if sanitize else "", os.getpid()))
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"] \
+        if sanitize else ["-O2"]
+    subprocess.run(["g++", *flags, "-std=c++17", "-ffp-contract=off", os.path.join(HERE, "cpp", "img_dump.cpp"), "-o",
                     exe, "-lz"], check=True)
+    return exe
+
+
+def _loader(exe):
 
     def run(path, raw, tmp):
         out = os.path.join(str(tmp), "dump.bin")
@@ -49,6 +54,19 @@ def load():
             px = np.frombuffer(f.read(), dtype=np.float32)
         return st, px.reshape(h, w, 4) if st == 0 else None
     return run
+
+
+@pytest.fixture(scope="module")
+def load():
+    return _loader(_harness(False))
+
+
+@pytest.fixture(scope="module")
+def load_asan():
+    """The same harness built with AddressSanitizer + UBSan (host code only):
+    a decoder that writes or reads out of bounds, or shifts by 32 or more,
+    aborts instead of passing."""
+    return _loader(_harness(True))
 
 
 def pil_rgb01(path):
@@ -206,3 +224,101 @@ def test_hdr_rejects_other_layouts(load, tmp_path):
     assert load(tmp_path / "y.hdr", False, tmp_path)[0] == 1
     (tmp_path / "z.hdr").write_bytes(_hdr_bytes(rgbe, "flat")[:-5])  # truncated scanline
     assert load(tmp_path / "z.hdr", False, tmp_path)[0] == 1
+
+
+# ---------------------------------------------------------------- malformed files (ASan + UBSan harness)
+def _segments(data):
+    """(marker, offset of the segment's payload, payload length) of a JPEG's header segments."""
+    out, pos = [], 2
+    while pos + 4 <= len(data) and data[pos] == 0xFF:
+        m = data[pos + 1]
+        if m == 0xDA:
+            break
+        ln = data[pos + 2] << 8 | data[pos + 3]
+        out.append((m, pos + 4, ln - 2))
+        pos += 2 + ln
+    return out
+
+
+def _dc_table(data):
+    """Payload offset of the first DC Huffman table (class 0) of a JPEG."""
+    for m, off, ln in _segments(data):
+        i = 0
+        while m == 0xC4 and i + 17 <= ln:
+            tc = data[off + i] >> 4
+            total = sum(data[off + i + 1: off + i + 17])
+            if tc == 0:
+                return off + i
+            i += 17 + total
+    raise AssertionError("no DC table")
+
+
+def test_jpeg_malformed_huffman_tables(load_asan, tmp_path):
+    good = tmp_path / "g.jpg"
+    _image(32, 24, 11, False).save(str(good), quality=85)
+    data = bytearray(good.read_bytes())
+    st, px = load_asan(good, True, tmp_path)
+    assert st == 0
+    np.testing.assert_array_equal(px[..., :3], pil_rgb01(good))
+    t = _dc_table(data)
+    counts = list(data[t + 1: t + 17])
+    # over-subscribed: three codes of length 1 (moved from a longer length, so
+    # the segment stays the same size) -- the table must be refused before its
+    # lookahead entries are written past the 512-entry arrays
+    for take_from in range(1, 16):
+        if counts[take_from] >= 3:
+            break
+    bad = bytearray(data)
+    bad[t + 1] = counts[0] + 3
+    bad[t + 1 + take_from] = counts[take_from] - 3
+    (tmp_path / "over.jpg").write_bytes(bytes(bad))
+    assert load_asan(tmp_path / "over.jpg", False, tmp_path)[0] == 1  # corrupt -> Image::EMPTY
+    # 255 codes of length 1: more symbols than the segment holds (short DHT)
+    bad = bytearray(data)
+    bad[t + 1] = 255
+    (tmp_path / "over255.jpg").write_bytes(bytes(bad))
+    assert load_asan(tmp_path / "over255.jpg", False, tmp_path)[0] == 1
+    # a DC symbol (difference bit count) above 15: refused as libjpeg refuses it
+    total = sum(counts)
+    for k in range(total):
+        bad = bytearray(data)
+        bad[t + 17 + k] = 0x20 + k
+        (tmp_path / "dc.jpg").write_bytes(bytes(bad))
+        assert load_asan(tmp_path / "dc.jpg", False, tmp_path)[0] == 1
+
+
+def test_png_and_hdr_limits(load_asan, tmp_path):
+    """A file past the library's 2^28-pixel limit is RT_EUNSUPPORTED (3) -- the
+    crate might decode it -- not Image::EMPTY; a bad signature is EMPTY (1)."""
+    import struct
+    import zlib
+
+    def chunk(t, d):
+        return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
+    big = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", 1 << 15, 1 << 14, 8, 2, 0, 0, 0)) + \
+        chunk(b"IDAT", zlib.compress(b"\x00" * 16)) + chunk(b"IEND", b"")
+    (tmp_path / "big.png").write_bytes(big)
+    assert load_asan(tmp_path / "big.png", False, tmp_path)[0] == 3
+    (tmp_path / "sig.png").write_bytes(b"\x89PNX\r\n\x1a\n" + big[8:])
+    assert load_asan(tmp_path / "sig.png", False, tmp_path)[0] == 1
+    (tmp_path / "big.hdr").write_bytes(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y 32768 +X 16384\n")
+    assert load_asan(tmp_path / "big.hdr", False, tmp_path)[0] == 3
+
+
+@pytest.mark.parametrize("chain", [4, 9, 40])
+def test_hdr_long_repeat_chain(load_asan, tmp_path, chain):
+    """Old-style RLE: each consecutive (1, 1, 1, n) marker shifts its count 8
+    bits further (Radiance's oldreadcolrs).  A chain long enough to shift a
+    nonzero count past 24 bits is corrupt; zero counts at any length are
+    harmless -- and no shift reaches 64 bits (UBSan)."""
+    w = 16
+    hdr = b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y 1 +X %d\n" % w
+    px = bytes([10, 20, 30, 130])
+    body = px + bytes([1, 1, 1, 1]) + bytes([1, 1, 1, 0]) * chain
+    (tmp_path / "zero.hdr").write_bytes(hdr + body + px * (w - 2))
+    st, out = load_asan(tmp_path / "zero.hdr", True, tmp_path)
+    assert st == 0 and out.shape == (1, w, 4)
+    body = px + bytes([1, 1, 1, 0]) * chain + bytes([1, 1, 1, 1])
+    (tmp_path / "big.hdr").write_bytes(hdr + body + px * (w - 2))
+    st, _ = load_asan(tmp_path / "big.hdr", True, tmp_path)
+    assert st == (0 if chain < 2 else 1)  # count 1 << (8 chain) > 16 pixels: corrupt

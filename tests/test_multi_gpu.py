@@ -136,3 +136,41 @@ def test_render_device_on_device_list(gpu, rt, scenes, capi):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), ref)
     assert st.n_devices == 2
+
+
+def test_two_threads_share_a_communicator(gpu, rt, scenes):
+    """Two scenes rendered at once from two host threads, both gathering
+    through one rt_comm: each gather's RCCL group is enqueued whole under the
+    communicator's lock, so every frame is its own scene's, bit-equal to a
+    render on one thread (ctypes releases the GIL inside the library)."""
+    import threading
+
+    jobs = [_scene(rt, scenes, gpu, 80, 9), _scene(rt, scenes, gpu, 72, 4)]
+    refs = [cam.render(world, lights, seed=30 + k, want_srgb=False)[0] for k, (s, world, lights, cam) in enumerate(jobs)]
+    uid = (ctypes.c_uint8 * 128)()
+    gpu.check(gpu.comm_unique_id(uid))
+    comm = gpu.comm_init(uid, 1, 0)
+    assert comm, gpu.last_error()
+    errors, frames = [], [[], []]
+
+    def worker(k):
+        try:
+            s, world, lights, cam = jobs[k]
+            for _ in range(6):
+                frames[k].append(cam.render(world, lights, seed=30 + k, want_srgb=False, comm=comm)[0])
+        except Exception as e:  # reported below, on the test's thread
+            errors.append(e)
+    try:
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in ts), "a render thread hung"
+        assert not errors, errors
+        for k in range(2):
+            assert len(frames[k]) == 6
+            for f in frames[k]:
+                np.testing.assert_array_equal(f, refs[k])
+    finally:
+        gpu.comm_destroy(comm)
