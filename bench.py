@@ -127,6 +127,67 @@ def _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads):
     return st.samples, time.perf_counter() - t0
 
 
+def physical_cores():
+    """{logical cpu: its core's sibling list} of the CPUs this process may run
+    on, from sysfs (None when the topology is not readable)."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+        sib = {}
+        for c in allowed:
+            txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+            cpus = []
+            for part in txt.split(","):
+                a, _, b = part.partition("-")
+                cpus.extend(range(int(a), int(b or a) + 1))
+            sib[c] = tuple(sorted(cpus))
+        return sib
+    except (OSError, ValueError):
+        return None
+
+
+def smt_yield(api, capi, scene, world, lights, cam, row_stride, budget):
+    """Measured SMT yield of the oracle: k threads pinned one per physical
+    core against 2k threads on the same k cores' two hardware threads each
+    (k = budget / 2, inside the job's CPU quota), on the same sample.  The
+    whole-host estimate scales the 2-thread-per-core rate by the host's
+    physical cores -- no assumption that a second hardware thread doubles a
+    core's rate."""
+    sib = physical_cores()
+    if not sib:
+        return None
+    cores, seen = [], set()
+    for c, s in sorted(sib.items()):
+        if s[0] not in seen and all(x in sib for x in s):
+            seen.add(s[0])
+            cores.append(s)
+    smt = sum(len(s) == 2 for s in cores) >= len(cores) // 2 and any(len(s) == 2 for s in cores)
+    if smt:
+        cores = [s for s in cores if len(s) == 2]
+    k = min(len(cores), max(1, budget // 2 if smt else budget))
+    pick = cores[:k]
+    saved = os.sched_getaffinity(0)
+    try:
+        os.sched_setaffinity(0, {s[0] for s in pick})
+        n1, dt1 = _oracle_render(api, capi, scene, world, lights, cam, row_stride, k)
+        n2, dt2 = n1, dt1
+        if smt:
+            os.sched_setaffinity(0, {x for s in pick for x in s})
+            n2, dt2 = _oracle_render(api, capi, scene, world, lights, cam, row_stride, 2 * k)
+    finally:
+        os.sched_setaffinity(0, saved)
+    r1, r2 = n1 / dt1 / 1e6, n2 / dt2 / 1e6
+    out = {"cores": k, "one_thread_per_core": round(r1, 4), "unit": "Msamples/s", "cpus": [list(s) for s in pick]}
+    if smt:
+        out.update({"two_threads_per_core": round(r2, 4), "yield": round(r2 / r1, 4),
+                    "sample": f"every {row_stride}th row; {k} threads pinned one per core ({dt1:.1f} s), then "
+                              f"{2 * k} threads on those cores' {2 * k} hardware threads ({dt2:.1f} s)"})
+    else:
+        out.update({"two_threads_per_core": None, "yield": None,
+                    "sample": f"every {row_stride}th row; {k} threads pinned one per core ({dt1:.1f} s); no SMT"})
+    out["per_core_busy"] = round(r2 / k, 5)
+    return out
+
+
 def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     """The TEST-ONLY oracle (reference algorithm, f64, recursive ray_color,
     reference BVH topology, pixels over `threads` host threads as rayon does)
@@ -162,17 +223,25 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     res["per_core"] = {"value": per_core, "unit": "Msamples/s", "seconds": round(dt1, 2), "samples": samples1,
                        "sample": f"1 thread, every {row_stride * max(1, threads)}th row at {spp} spp"}
     res["host"] = topo
-    hw_threads = topo.get("CPU(s)") if isinstance(topo.get("CPU(s)"), int) else None
-    if hw_threads:
-        # labelled extrapolation, never the measured baseline: the measured
-        # per-thread rate of the `threads`-thread run times every hardware
-        # thread of the host (linear scaling, as rayon over pixels would
-        # approach on an idle host)
-        res["whole_host_extrapolated"] = {
-            "value": res["value"] / threads * hw_threads, "unit": "Msamples/s", "threads": hw_threads,
-            "basis": f"EXTRAPOLATED, not measured: {res['value']:.3f} Msamples/s on {threads} threads x "
-                     f"{hw_threads}/{threads} ({topo.get('Socket(s)')} sockets x {topo.get('Core(s) per socket')} "
-                     f"cores x {topo.get('Thread(s) per core')} threads)"}
+    # the whole host (every physical core, both hardware threads), ESTIMATED
+    # from the measured SMT rate per core: k cores, two threads each, on the
+    # same rows as the measured baseline (per-row cost varies: sky rows are
+    # cheap), times the host's physical cores
+    smt = smt_yield(api, capi, scene, world, lights, cam, row_stride, threads)
+    res["smt"] = smt
+    phys = None
+    if isinstance(topo.get("Socket(s)"), int) and isinstance(topo.get("Core(s) per socket"), int):
+        phys = topo["Socket(s)"] * topo["Core(s) per socket"]
+    if smt and phys:
+        per_core_smt = smt["per_core_busy"]
+        res["whole_host_estimated"] = {
+            "value": round(per_core_smt * phys, 3), "unit": "Msamples/s", "physical_cores": phys,
+            "hw_threads": topo.get("CPU(s)"),
+            "basis": f"ESTIMATED, not measured: {per_core_smt:.4f} Msamples/s per physical core with both hardware "
+                     f"threads busy (measured on {smt['cores']} cores, SMT yield {smt['yield']}) x {phys} "
+                     f"physical cores ({topo.get('Socket(s)')} sockets x {topo.get('Core(s) per socket')}); "
+                     "assumes every core of the node runs at the measured per-core rate (no memory-bandwidth or "
+                     "clock loss when all are busy)"}
     if workload == "c2":
         s1 = rt.Scene(api)
         w1, l1, cam1 = scenes.random_spheres(s1, 400, 100)
@@ -419,6 +488,14 @@ def main():
                                    "counters x this launch's samples)") if traffic_src else None,
             },
         }
+        if traffic:
+            gbs = traffic / (kernel_avg_ms * 1e-3) / 1e9
+            line["roofline"]["hbm_gbs"] = round(gbs, 3)
+            line["roofline"]["hbm_peak_gbs"] = HBM_PEAK_GBS
+            line["roofline"]["hbm_frac"] = round(gbs / HBM_PEAK_GBS, 6)
+            line["roofline"]["hbm_note"] = ("traffic / path-kernel time; the read bytes are L2 miss requests "
+                                            "(TCC_EA0_RDREQ_*), which also count Infinity Cache (MALL) hits: an upper "
+                                            "bound on DRAM bytes")
         if exec_fps:
             ach_e = exec_fps * launch_samples / (kernel_avg_ms * 1e-3) / 1e12
             line["roofline"]["achieved_executed"] = round(ach_e, 4)
@@ -449,7 +526,13 @@ def main():
             threads, info = usable_cpus()
             if args.cpu_threads:
                 threads = args.cpu_threads
-            line["cpu_baseline"] = cpu_baseline(threads, args.cpu_row_stride, cpu_spp, args.workload, info)
+            cb = cpu_baseline(threads, args.cpu_row_stride, cpu_spp, args.workload, info)
+            # the north-star ratios, GPU value over each CPU rate (vs_baseline
+            # stays the driver's: BASELINE.md holds no published number)
+            cb["speedup"] = round(value / cb["value"], 2)
+            if cb.get("whole_host_estimated"):
+                cb["speedup_whole_host"] = round(value / cb["whole_host_estimated"]["value"], 2)
+            line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     if comm:
         api.comm_destroy(comm)

@@ -1728,8 +1728,22 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
 
-#ifndef RT_HOIST_DRAWS
-#define RT_HOIST_DRAWS 1
+// Basic / mesh tiers: the draws of one path vertex that every scattering
+// material there takes -- slots 0 and 1 of the vertex (one Philox block) and
+// cos / sin(2 pi xi0) (Lambertian's cosine direction and Metal's
+// random_unit_vector, vec3.rs:313-343; Dielectric's Schlick draw is xi0) --
+// made once per wave iteration by the main loop, shared with the camera rays
+// of the lanes that start a sample there (random_in_unit_disk's theta is
+// 2 pi xi too, vec3.rs:63-69): one Philox block and one sincos per lane and
+// iteration instead of a shading set and a camera set.
+struct Draws {
+    double xi0, xi1, sn, cs;
+};
+// Tiers (bit 0 basic, bit 1 mesh) whose main loop shares the draws.  A/B
+// (RMSE 0): C2 -1.3 % (64 spp) / -1.8 % (128 spp) kernel time; the mesh tier
+// +3.3 % on C4 (64 spp): there the loop's extra live state spills 44 B/lane.
+#ifndef RT_UNIFIED_DRAWS
+#define RT_UNIFIED_DRAWS 1
 #endif
 
 // ---- general materials (tier FULL_GL): DiffuseLight / Mix wrappers nested
@@ -1766,7 +1780,7 @@ __device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p
 // true when the path ends here (miss, no scatter, panic).
 template <int TIER>
 __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
-                                      const HitInfo& h, bool& panic) {
+                                      const HitInfo& h, bool& panic, const Draws& Dr = Draws{}) {
     constexpr bool FULL = tier_full(TIER);
     constexpr bool PL = tier_full_bvh(TIER) && RT_PERLIN_LDS;  // the flat tier's LDS is full
     uint32_t ovf = 0;
@@ -1792,15 +1806,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     DMaterial M = S.materials[rec.mat];
     // Basic / mesh tiers: every scattering material draws slot 0 (and 1) of
     // this vertex first, and Lambertian and Metal both turn the first draw
-    // into cos/sin(2 pi r1) (vec3.rs:313-322, 333-343).  Drawn once here for
-    // the whole wave instead of once per material branch a lane takes.
-    constexpr bool HOIST = !FULL && RT_HOIST_DRAWS;
-    double xi0 = 0.0, xi1 = 0.0, sn0 = 0.0, cs0 = 0.0;
-    if constexpr (HOIST) {
-        xi0 = rng.next(ovf);
-        xi1 = rng.next(ovf);
-        k_sincos(2.0 * PI * xi0, &sn0, &cs0);
-    }
+    // into cos/sin(2 pi r1) (vec3.rs:313-322, 333-343): the main loop's Draws.
+    constexpr bool HOIST = !FULL;
+    const double xi0 = Dr.xi0, xi1 = Dr.xi1, sn0 = Dr.sn, cs0 = Dr.cs;
     if constexpr (TIER == TIER_FULL_GL) {
         if (M.flags & MF_EMISSIVE) L = L + beta * emitted_tree<RT_MAT_DEPTH>(S, rec.mat, rec.u, rec.v, rec.p);
         // the wrappers' scatter: DiffuseLight -> its material or None, Mix -> one draw (material.rs:180-185, 254-260)
@@ -2132,6 +2140,215 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     uint32_t trace_items = 0, trace_q = 0, trace_rays = 0, trace_steps = 0, trace_steps_q = 0;
     unsigned long long trace_tq = trace_t0;
 #endif
+    // ---- refill: the lanes that need a queue entry take one (false: the
+    // queue is done and this lane leaves the loop)
+    auto refill = [&]() -> bool {
+        // wave-aggregated dequeue of stratum rows.  The wave takes
+        // RT_QUEUE_CHUNK items per atomic into a wave-uniform pool and hands them
+        // to its lanes in rank order: one contended atomic per chunk, not one per
+        // main-loop iteration (every iteration some lane of the wave needs work).
+        const unsigned long long mask = __ballot(need);
+        if (mask) {
+            const uint32_t n = (uint32_t)__popcll(mask);
+            const uint32_t avail = pool_end - pool_next;
+            uint32_t fresh = 0;
+            // guided chunk: about 1/GUIDE of the items left (as last seen) per
+            // wave of the grid, so the last chunks are small and waves finish
+            // together; never below what the wave's lanes need now, nor below
+            // Frame::chunk_min.  Near the end a wave takes only what its lanes
+            // need: a pool held by a slow wave (deep glass paths) is work the
+            // idle waves cannot take (scripts/lane_trace.py).
+            uint32_t chunk = RT_QUEUE_CHUNK;
+#if RT_QUEUE_GUIDE
+            {
+                // the work left in part-sized entries (a whole-row entry is
+                // `parts` of them), and the chunk in the entries it takes: a
+                // pool of whole rows taken as the tail starts is no larger
+                // in samples than the tail's pools (it would outlast them)
+                const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
+                const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
+                const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
+                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), F.chunk_cap);
+                chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
+            }
+#endif
+            if (avail < n) {
+                if (!dry) {
+                    const uint32_t leader = __ffsll((long long)mask) - 1;
+                    if (lane == leader) fresh = atomicAdd(queue, chunk);
+                    fresh = __shfl(fresh, leader) + F.static_entries;
+                    dry = fresh + chunk >= F.queue_total;
+                } else {
+                    fresh = F.queue_total;  // past the end: the needy lanes leave
+                }
+            }
+            const uint32_t old_next = pool_next;
+            if (avail < n) {
+                pool_next = fresh + (n - avail);
+                pool_end = fresh + chunk;
+            } else {
+                pool_next += n;
+            }
+            if (need) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                const uint32_t q = rank < avail ? old_next + rank : fresh + (rank - avail);
+                if (q >= F.queue_total) return false;
+                need = false;
+#ifdef RT_WAVE_TRACE
+                ++trace_items;
+                trace_q = q;
+                trace_rays = n_rays;
+                trace_steps_q = trace_steps;
+                trace_tq = __builtin_amdgcn_s_memrealtime();
+#endif
+                const bool whole = q < F.whole_items;
+                const uint32_t qt = whole ? 0u : q - F.whole_items;  // (udiv_inv wants n < 2^32 in range)
+                const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
+                const uint32_t item = whole ? q : F.whole_items + it;
+                s_j = whole ? 0u : part * F.part_len;
+                acc = d3(0, 0, 0);
+                const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
+                sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
+                slot = q;
+                const uint32_t prow = udiv_inv(pl, F.inv_W);
+                rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
+            }
+        }
+        return true;
+    };
+    // ---- the end of a lane's sample (camera.rs:193's sum, in s_j order): its
+    // radiance joins the entry's sum; the entry's last sample writes the sum
+    auto finish_sample = [&]() {
+        if (isnan(L.x) || isnan(L.y) || isnan(L.z)) {  // camera.rs:323
+            ++n_panics;
+            L = d3(0, 0, 0);
+        }
+        acc = acc + L;
+        ++s_j;
+        if (s_j == (sie >> 16)) {
+            double* dst = P->partial + (uint64_t)slot * 3;
+            dst[0] = acc.x;
+            dst[1] = acc.y;
+            dst[2] = acc.z;
+            need = true;
+        }
+    };
+    if constexpr (!tier_full(TIER) && ((RT_UNIFIED_DRAWS >> TIER) & 1)) {
+        // Basic / mesh tiers: a lane's iteration is walk -> (miss: the sample
+        // ends) -> refill -> draws -> shade or a new sample's camera ray, so
+        // that the one Philox block and sincos of the iteration's Draws serve
+        // both (struct Draws).  A lane whose path ends in shading (depth,
+        // panic, no scatter) starts its next sample one iteration later.
+        bool no_path = true;  // the lane starts a sample at its next post-walk stage
+        constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC : RT_SHADE_BATCH_MESH;
+        for (;;) {
+            RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
+            if (!no_path) {
+                if (!walking) {
+                    rng.begin(vertex);
+                    ++n_rays;
+                    trace_begin<TIER>(S, ray, T);
+                    walking = true;
+                } else if constexpr (PARK) {
+                    trace_unpark(ray, T, pk);  // a walk carried over the last shading round
+                }
+            }
+            RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
+            auto step = [&]() -> bool {
+                if constexpr (TIER == TIER_BASIC && RT_BVH4) {
+                    return trace4_step(S, ray, T, stk, pq, (const RT_LDS float4*)node_lds, dg);
+                } else {
+                    RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters; ++dg.lane_trace_iters;)
+                    return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
+                }
+            };
+            if constexpr (BATCH >= 64) {
+#ifdef RT_WAVE_TRACE
+                while (walking) walking = step(), ++trace_steps;
+#else
+                while (walking) walking = step();
+#endif
+            } else {
+                const unsigned long long active = __ballot(true);
+                for (;;) {
+                    if (walking) walking = step();
+                    const unsigned long long w = __ballot(walking);
+                    if (w == 0 || __popcll(active & ~w) >= BATCH) break;
+                }
+            }
+            RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
+            // a walk that carries over this shading round (mesh tier) is parked;
+            // the lane skips the rest of the iteration but for the refill,
+            // which every lane of the wave runs: the queue pool (pool_next,
+            // pool_end, dry) is wave-uniform state and must be updated in
+            // uniform control flow, or a parked lane would keep a stale copy
+            const bool carry = BATCH < 64 && walking;
+            if constexpr (PARK) {
+                if (carry) trace_park(T, pk);
+            }
+            // ---- this lane's walk is over, or it has no path
+            bool cam = no_path;
+            if (!carry && !no_path && !T.found) {  // a miss: Environment::value, and the sample ends
+                bool panic = false;
+                shade<TIER>(S, ray, beta, L, rng, false, T.hit, panic);
+                if (panic) ++n_panics;
+                finish_sample();
+                cam = true;
+            }
+            if (!refill()) break;
+            if (carry) continue;
+            // the iteration's draws: a hit's (vertex, slots 0 and 1) or a new
+            // sample's camera draws (vertex 0: theta and r of the defocus disk
+            // at slots 2 and 3, else the pixel offsets at slots 0 and 1)
+            if (cam) rng.sample = (sie & 0xFFFFu) * F.S + s_j;
+            Draws Dr;
+            rng.pair(cam ? 0u : vertex, (cam && F.defocus) ? 1u : 0u, Dr.xi0, Dr.xi1);
+            k_sincos(2.0 * PI * Dr.xi0, &Dr.sn, &Dr.cs);
+            RT_DIAG_ONLY(const unsigned long long t_d = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_d - t_b1;)
+            if (!cam) {
+                // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
+                rng.begin(vertex);
+                rng.slot = 2;  // slots 0 and 1 are Dr
+                bool panic = false;
+                bool end_path = shade<TIER>(S, ray, beta, L, rng, true, T.hit, panic, Dr);
+                if (panic) {
+                    ++n_panics;
+                    end_path = true;
+                }
+                if (!end_path) {
+                    ++vertex;
+                    if (vertex > F.max_depth) end_path = true;  // depth == 0 -> BLACK (camera.rs:282-284)
+                }
+                if (end_path) {
+                    finish_sample();
+                    no_path = true;
+                }
+                RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_d;)
+            } else {
+                // ---- Camera::get_ray (camera.rs:247-273), vertex 0
+                const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
+                double xi0 = Dr.xi0, xi1 = Dr.xi1;
+                D3 origin = F.center;
+                if (F.defocus) {  // vec3.rs:63-69: theta = 2 pi Dr.xi0, r = sqrt(Dr.xi1)
+                    rng.pair(0u, 0u, xi0, xi1);
+                    const double rr = sqrt(Dr.xi1);
+                    origin = (F.center + ((rr * Dr.cs) * F.disk_u)) + ((rr * Dr.sn) * F.disk_v);
+                }
+                const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
+                const double oy = (((double)s_j + xi1) * F.recip_sqrt_spp) - 0.5;
+                const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
+                ray.o = origin;
+                ray.d = ps - origin;
+                ray.time = 0.0;  // read only by moving spheres (full tiers): its draw is skipped
+                beta = d3(1, 1, 1);
+                L = d3(0, 0, 0);
+                vertex = 1;
+                no_path = false;
+                RT_DIAG_ONLY(dg.cyc_refill += __builtin_amdgcn_s_memtime() - t_d;)
+            }
+        }
+    } else {
     for (;;) {
         RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
         // ---- refill: wave-aggregated dequeue of stratum rows.  The wave takes
@@ -2313,7 +2530,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             continue;
         }
         bool panic = false;
-        bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic);
+        Draws Dr{};
+        if constexpr (!tier_full(TIER)) {  // (RT_UNIFIED_DRAWS off: the shading draws made here)
+            if (T.found) {
+                uint32_t ovf = 0;
+                Dr.xi0 = rng.next(ovf);
+                Dr.xi1 = rng.next(ovf);
+                k_sincos(2.0 * PI * Dr.xi0, &Dr.sn, &Dr.cs);
+            }
+        }
+        bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic, Dr);
         RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_b1;)
         if (panic) {
             ++n_panics;
@@ -2340,6 +2566,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             }
         }
     }
+    }  // full tiers
 #ifdef RT_DIAG
     // wave-uniform cycle counts: lane 0 of each wave; lane counters: every lane
     if (lane == 0) {

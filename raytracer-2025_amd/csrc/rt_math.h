@@ -120,6 +120,14 @@ struct Rng {
         ++slot;
         return r;
     }
+    // draws 2p and 2p + 1 of vertex v (one Philox block), as next() would
+    // return them at slots 2p and 2p + 1; the stream position is not moved
+    __device__ __forceinline__ void pair(uint32_t v, uint32_t p, double& a, double& b) const {
+        uint32_t c0 = v * 8u + p, c1 = pixel, c2 = sample, c3 = 0u;
+        philox4x32_10(c0, c1, c2, c3, k0, k1);
+        a = u64_unit(c0, c1);
+        b = u64_unit(c2, c3);
+    }
     __device__ __forceinline__ double medium(uint32_t id) const {
         uint32_t c0 = vertex, c1 = pixel, c2 = sample, c3 = 1u + id;
         philox4x32_10(c0, c1, c2, c3, k0, k1);

@@ -41,10 +41,20 @@ def test_bench_line_contract():
     assert rf["peak"] == 78.6 and rf["unit"] == "TFLOP/s"
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
     assert 0 < rf["kernel_ms_avg"] <= d["ms_per_step"] * 1.05
+    if rf["traffic"] is not None:  # HBM bytes from the committed PMC summary: the GB/s view of them
+        assert rf["hbm_peak_gbs"] == 8000.0
+        assert abs(rf["hbm_gbs"] - rf["traffic"] / (rf["kernel_ms_avg"] * 1e-3) / 1e9) <= 1e-3 * rf["hbm_gbs"] + 1e-3
+        assert abs(rf["hbm_frac"] - rf["hbm_gbs"] / 8000.0) < 1e-5
     cb = d["cpu_baseline"]
-    for k in ("value", "unit", "cores", "kind", "sample"):
+    for k in ("value", "unit", "cores", "kind", "sample", "speedup", "smt"):
         assert k in cb, k
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+    assert abs(cb["speedup"] - d["value"] / cb["value"]) <= 0.01 * cb["speedup"] + 0.01
+    if cb["smt"]:  # SMT yield measured on the box's own cores, not assumed
+        assert cb["smt"]["one_thread_per_core"] > 0 and cb["smt"]["per_core_busy"] > 0
+        whole = cb["whole_host_estimated"]
+        assert whole["value"] > 0 and "ESTIMATED" in whole["basis"]
+        assert abs(cb["speedup_whole_host"] - d["value"] / whole["value"]) <= 0.01 * cb["speedup_whole_host"] + 0.01
 
 
 def test_bench_two_ranks_gloo():
