@@ -470,7 +470,37 @@ struct StackB4 {
         const uint32_t e = base[sp * BLK], r16 = e >> 16;
         return make_uint2(make_ref((r16 & 0x8000u) ? K_LIST : K_BVH, r16 & 0x7fffu), e << 16);
     }
+    // The 4-wide basic tier's walk keeps its refs as "words" (bword): a
+    // box child's 16-bit stack code in the upper half -- push is one byte
+    // permute with the entry distance, pop one mask
+    __device__ __forceinline__ void push_w(uint32_t sp, uint32_t word, float t) {
+        base[sp * BLK] = __builtin_amdgcn_perm(word, __float_as_uint(t), 0x07060302u);
+    }
+    __device__ __forceinline__ uint2 at_w(uint32_t sp) const {
+        const uint32_t e = base[sp * BLK];
+        return make_uint2(e & 0xffff0000u, e << 16);
+    }
 };
+// Basic-tier walk words (the 4-wide walk's cur, stack entries and the ref
+// row of the block's LDS node copy): 0 = none; a node = (index + 1) << 16;
+// a list position = (0x8000 | index) << 16; a sphere = 0x8000 | index (low
+// half).  So a box child is word > 0xffff, a sphere child has a nonzero low
+// half, and the upper half is the stack entry's ref code as it stands.
+// Indices: nodes < 0x7fff (the LDS copy holds 658), lists < 0x8000 and
+// spheres < 0x8000 (rt_render.cpp prepare_tier).
+__device__ __forceinline__ uint32_t bword(const SceneView& S, uint32_t ref) {
+    const uint32_t k = ref_kind(ref), i = ref_idx(S, ref);
+    return k == K_BVH ? (i + 1u) << 16 : k == K_LIST ? (0x8000u | i) << 16 : k == K_SPHERE ? (0x8000u | i) : 0u;
+}
+template <class Stack>
+__device__ __forceinline__ uint32_t pop_w(const Stack& stk, uint32_t& sp, float c_f) {
+    while (sp > 0) {
+        --sp;
+        const uint2 e = stk.at_w(sp);
+        if (__uint_as_float(e.y) <= c_f) return e.x;
+    }
+    return 0u;
+}
 template <int TIER, bool B4 = TIER == TIER_BASIC && RT_STACK4B>
 struct StackSel {
     using type = StackT<lds_stack_entries(TIER), TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
@@ -857,6 +887,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
         const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
         T.sf = make_sphf(o, d);
         T.pn = 0;
+        T.cur = bword(S, S.world_root);  // the 4-wide walk's cur is a walk word
     }
 }
 
@@ -1180,9 +1211,6 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #endif
 
 // ------------------------------------------------------------------ basic tier: 4-wide BVH
-#ifndef RT_SLOT_BALLOT
-#define RT_SLOT_BALLOT 1
-#endif
 // One visit of a DNode4: the sphere children's f32 filter (queued into the
 // lane's LDS queue, pq[k * RT_BLOCK_BASIC], when the exact test must run), then the
 // four slab tests; the hit boxes are sorted by entry distance, the nearest is
@@ -1200,7 +1228,7 @@ __device__ __forceinline__ Node4Rows load_node4(const RT_LDS float4* nl, uint32_
     const RT_LDS float4* np = nl + idx * 7u;
     return Node4Rows{np[0], np[1], np[2], np[3], np[4], np[5], np[6]};
 }
-// visit4 on node rows already loaded
+// visit4 on node rows already loaded; the ref row holds walk words (bword)
 template <class Stack>
 __device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4Rows& nr, const RayF& rf, const SphF& sf, float tmin_f,
                                                 float& c_f, Stack& stk, uint32_t& sp, RT_LDS uint16_t* pq, uint32_t& pn) {
@@ -1208,28 +1236,25 @@ __device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4R
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, LY[4] = {ly.x, ly.y, ly.z, ly.w}, LZ[4] = {lz.x, lz.y, lz.z, lz.w};
     const float HX[4] = {hx.x, hx.y, hx.z, hx.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
     const uint32_t R[4] = {__float_as_uint(rq.x), __float_as_uint(rq.y), __float_as_uint(rq.z), __float_as_uint(rq.w)};
-    bool sph[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sph[i] = ref_kind(R[i]) == K_SPHERE;
     constexpr float INF = __builtin_huge_valf();
     float key[4];
     uint32_t ref[4];
-#if RT_SLOT_BALLOT
     // per slot, the filter / slab only when some lane has a sphere / a box
     // there: the flatten puts a node's spheres in its low slots and its empty
     // slots last (rth::bvh4_convert), and most leaf-level nodes hold 2-3 spheres
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        if (__ballot(sph[i])) {
-            if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
-                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_idx(S, R[i]);
+        bool sph = (uint16_t)R[i] != 0;
+        if (__ballot(sph)) {
+            if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph)) {
+                pq[pn * RT_BLOCK_BASIC] = (uint16_t)(R[i] & 0x7fffu);
                 ++pn;
             }
         }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const bool box = R[i] != REF_NONE && !sph[i];
+        const bool box = R[i] > 0xffffu;
         key[i] = INF;
         ref[i] = R[i];
         if (__ballot(box)) {
@@ -1239,25 +1264,6 @@ __device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4R
             key[i] = h ? e : INF;
         }
     }
-#else
-    if (__ballot(sph[0] || sph[1] || sph[2] || sph[3])) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (sphere_filter(LX[i], LY[i], LZ[i], HX[i], HY[i], sf, c_f, sph[i])) {
-                pq[pn * RT_BLOCK_BASIC] = (uint16_t)ref_idx(S, R[i]);
-                ++pn;
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float lo[3] = {LX[i], LY[i], LZ[i]}, hi[3] = {HX[i], HY[i], HZ[i]};
-        float e;
-        const bool h = slab_f(lo, hi, rf, tmin_f, c_f, e) && R[i] != REF_NONE && !sph[i];
-        key[i] = h ? e : INF;
-        ref[i] = R[i];
-    }
-#endif
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];
@@ -1272,10 +1278,10 @@ __device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4R
     cs(0, 2);
     cs(1, 3);
     cs(1, 2);
-    if (key[3] < INF) stk.push(sp++, ref[3], key[3]);
-    if (key[2] < INF) stk.push(sp++, ref[2], key[2]);
-    if (key[1] < INF) stk.push(sp++, ref[1], key[1]);
-    return key[0] < INF ? ref[0] : REF_NONE;
+    if (key[3] < INF) stk.push_w(sp++, ref[3], key[3]);
+    if (key[2] < INF) stk.push_w(sp++, ref[2], key[2]);
+    if (key[1] < INF) stk.push_w(sp++, ref[1], key[1]);
+    return key[0] < INF ? ref[0] : 0u;
 }
 
 // One visit of a DNode4 whose children all carry boxes (mesh tier): four slab
@@ -1358,7 +1364,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     // round and issued first: its sphere load goes out before the node's
     // seven loads (loads complete in order), and its f64 test runs while the
     // node is in flight.
-    const bool can = (T.cur != REF_NONE || T.sp > 0) && pn <= ROOM;
+    const bool can = (T.cur != 0u || T.sp > 0) && pn <= ROOM;
     const unsigned long long mw0 = __ballot(can);
     const unsigned long long mp0 = __ballot(pn > 0);
 #if RT_DEFER_REL
@@ -1380,20 +1386,22 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     if (can) {
         RT_DIAG_ONLY(++dg.lane_trace_iters;)
 #ifdef RT_DIAG
-        if (T.cur == REF_NONE) {
+        if (T.cur == 0u) {
             const uint32_t sp_before = T.sp;
-            T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+            T.cur = pop_w(stk, T.sp, T.cl.c_f);
             ++dg.pops;
             dg.pop_reads += sp_before - T.sp;
         }
 #else
-        if (T.cur == REF_NONE) T.cur = pop(stk, T.sp, 0, T.cl.c_f);
+        if (T.cur == 0u) T.cur = pop_w(stk, T.sp, T.cl.c_f);
 #endif
         cur = T.cur;
-        T.cur = REF_NONE;
+        T.cur = 0u;
     }
-    const uint32_t kind = ref_kind(cur), idx = ref_idx(S, cur);
-    const Node4Rows rows = load_node4(nl, kind == K_BVH ? idx : 0u);
+    // cur is a walk word (bword): a node, a list position or a sphere
+    const uint32_t r16 = cur >> 16;
+    const bool node = r16 - 1u < 0x7fffu;  // 1 ..= 0x7fff
+    const Node4Rows rows = load_node4(nl - 7, node ? r16 : 1u);
     if (round) {  // sphere round (sphere.rs:77-108)
         RT_DIAG_ONLY(++dg.sphere_tests;)
         double t;
@@ -1406,24 +1414,25 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
             T.hit.ref = make_ref(K_SPHERE, sidx);
         }
     }
-    if (__ballot(kind != K_BVH && kind != K_NONE)) {  // lists, standalone spheres (none in C2)
-        if (kind == K_LIST) {
-            const uint32_t child = S.list_children[idx];
+    if (__ballot(!node && cur != 0u)) {  // lists, standalone spheres (none in C2)
+        if (r16 >= 0x8000u) {  // a list position
+            const uint32_t li = r16 & 0x7fffu;
+            const uint32_t child = S.list_children[li];
             if (child != REF_NONE) {
-                if (S.list_children[idx + 1] != REF_NONE) stk.push(T.sp++, make_ref(K_LIST, idx + 1), NO_CULL);
-                T.cur = child;
+                if (S.list_children[li + 1] != REF_NONE) stk.push_w(T.sp++, (0x8000u | (li + 1)) << 16, NO_CULL);
+                T.cur = bword(S, child);
             }
-        } else if (kind == K_SPHERE) {
-            pq[pn * RT_BLOCK_BASIC] = (uint16_t)idx;
+        } else {  // a sphere element of a list: queued for its exact test
+            pq[pn * RT_BLOCK_BASIC] = (uint16_t)(cur & 0x7fffu);
             ++pn;
         }
     }
-    if (kind == K_BVH) {
+    if (node) {
         RT_DIAG_ONLY(++dg.node_visits;)
         T.cur = visit4_rows(S, rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
     }
     T.pn = pn;
-    return T.cur != REF_NONE || T.sp > 0 || pn > 0;
+    return T.cur != 0u || T.sp > 0 || pn > 0;
 }
 
 // ------------------------------------------------------------------ hit record
@@ -2084,7 +2093,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     if constexpr (TIER == TIER_BASIC && RT_BVH4) {
         const uint32_t n_lds = min(S.n_nodes4, NODE_LDS_CAP);  // == n_nodes4 (launcher)
         const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
-        for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) node_lds[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) {
+            float4 v = src[k];
+            if (k % 7u == 6u) {  // the ref row: walk words (bword)
+                v.x = __uint_as_float(bword(S, __float_as_uint(v.x)));
+                v.y = __uint_as_float(bword(S, __float_as_uint(v.y)));
+                v.z = __uint_as_float(bword(S, __float_as_uint(v.z)));
+                v.w = __uint_as_float(bword(S, __float_as_uint(v.w)));
+            }
+            node_lds[k] = v;
+        }
         __syncthreads();
     }
     if constexpr (tier_full_bvh(TIER) && RT_PERLIN_LDS) {

@@ -257,8 +257,8 @@ void destroy_render_state(RenderState* r) {
 // -1 with RT_ESTACK set).
 static int prepare_tier(HostWorld& hw) {
     int tier = rtk_tier_for(hw.features, hw.stack_need);
-    // the basic tier queues sphere indices as 16-bit LDS entries
-    if (tier == rtk::TIER_BASIC && hw.spheres.size() > 65536) tier = rtk::TIER_MESH;
+    // the basic tier's walk words hold 15-bit sphere indices (rt_kernel.hip bword)
+    if (tier == rtk::TIER_BASIC && hw.spheres.size() > 32768) tier = rtk::TIER_MESH;
     // and its 4-B stack entries hold 15-bit node / list indices
     if (tier == rtk::TIER_BASIC && hw.list_children.size() >= 32768) tier = rtk::TIER_MESH;
     // the basic tier's kernel reads every 4-wide node from its LDS copy
