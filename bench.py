@@ -145,6 +145,31 @@ def physical_cores():
         return None
 
 
+def cpu_busy(interval=1.0):
+    """{cpu: busy fraction over `interval` s} from /proc/stat (None if unreadable)."""
+    def snap():
+        out = {}
+        for line in open("/proc/stat"):
+            if line.startswith("cpu") and line[3:4].isdigit():
+                f = line.split()
+                v = list(map(int, f[1:]))
+                idle = v[3] + (v[4] if len(v) > 4 else 0)
+                out[int(f[0][3:])] = (sum(v), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(interval)
+        b = snap()
+    except (OSError, ValueError):
+        return None
+    res = {}
+    for c in b:
+        if c in a:
+            dt = b[c][0] - a[c][0]
+            res[c] = 1.0 - (b[c][1] - a[c][1]) / dt if dt > 0 else 1.0
+    return res
+
+
 def smt_yield(api, capi, scene, world, lights, cam, row_stride, budget):
     """Measured SMT yield of the oracle: k threads pinned one per physical
     core against 2k threads on the same k cores' two hardware threads each
@@ -155,11 +180,16 @@ def smt_yield(api, capi, scene, world, lights, cam, row_stride, budget):
     sib = physical_cores()
     if not sib:
         return None
+    # the least busy physical cores (a GPU box's job shares its host: the
+    # low-numbered cores carry the system's and other jobs' threads)
+    busy = cpu_busy()
     cores, seen = [], set()
     for c, s in sorted(sib.items()):
         if s[0] not in seen and all(x in sib for x in s):
             seen.add(s[0])
             cores.append(s)
+    if busy:
+        cores.sort(key=lambda s: (max(busy.get(x, 1.0) for x in s), s[0]))
     smt = sum(len(s) == 2 for s in cores) >= len(cores) // 2 and any(len(s) == 2 for s in cores)
     if smt:
         cores = [s for s in cores if len(s) == 2]
@@ -176,7 +206,8 @@ def smt_yield(api, capi, scene, world, lights, cam, row_stride, budget):
     finally:
         os.sched_setaffinity(0, saved)
     r1, r2 = n1 / dt1 / 1e6, n2 / dt2 / 1e6
-    out = {"cores": k, "one_thread_per_core": round(r1, 4), "unit": "Msamples/s", "cpus": [list(s) for s in pick]}
+    out = {"cores": k, "one_thread_per_core": round(r1, 4), "unit": "Msamples/s", "cpus": [list(s) for s in pick],
+           "busy_before": [round(max(busy.get(x, 0.0) for x in s), 3) for s in pick] if busy else None}
     if smt:
         out.update({"two_threads_per_core": round(r2, 4), "yield": round(r2 / r1, 4),
                     "sample": f"every {row_stride}th row; {k} threads pinned one per core ({dt1:.1f} s), then "

@@ -29,6 +29,8 @@
 #pragma once
 #include <cmath>
 
+#include "rt_slab.h"  // rcp_f32, RT_RCP_F32
+
 #if defined(__HIPCC__)
 #define RT_HD __host__ __device__ __forceinline__
 #else
@@ -56,8 +58,19 @@ RT_HD SphF make_sphf(const double o[3], const double d[3]) {
     F.a = fmaf(F.d[2], F.d[2], fmaf(F.d[1], F.d[1], F.d[0] * F.d[0]));
     F.gr = (fabsf(F.o[0]) + fabsf(F.o[1]) + fabsf(F.o[2])) * (1.0f + 0x1p-20f);
     F.ka = F.a * 0x1p-17f;
+#if RT_RCP_F32 == 2
+    // the hardware square root and reciprocal (1 ulp): ehd's 2^-19 is five
+    // times the 6.2u bound it scales, and ia's margin of 2^-19 is 16 ulps
+#if defined(__HIP_DEVICE_COMPILE__)
+    F.ehd = __builtin_amdgcn_sqrtf(F.a) * 0x1p-19f;
+#else
+    F.ehd = std::sqrt(F.a) * 0x1p-19f;
+#endif
+    F.ia = rcp_f32(F.a) * (1.0f + 0x1p-19f);
+#else
     F.ehd = sqrtf(F.a) * 0x1p-19f;
     F.ia = (1.0f / F.a) * (1.0f + 0x1p-19f);
+#endif
     return F;
 }
 

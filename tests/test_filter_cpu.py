@@ -17,22 +17,25 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
 
 
-def build(contract):
+def build(contract, rcp=""):
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "filter_prop_%s.%d" % (contract, os.getpid()))  # one per pytest worker
+    exe = os.path.join(BUILD, "filter_prop_%s%s.%d" % (contract, rcp, os.getpid()))  # one per pytest worker
     exact = os.path.join(BUILD, "sphere_exact.o")
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-c", os.path.join(HERE, "cpp", "sphere_exact.cpp"),
                     "-o", exact], check=True)
     flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
+    if rcp:  # the hardware reciprocal of RT_RCP_F32 = 2, emulated an ulp up / down (rt_slab.h rcp_f32)
+        flags += ["-DRT_RCP_F32=2", "-DRT_RCP_EMU=%d" % (1 if rcp == "up" else -1)]
     subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "filter_prop.cpp"), exact, "-o", exe],
                    check=True)
     return exe
 
 
+@pytest.mark.parametrize("rcp", ["", "up", "down"])
 @pytest.mark.parametrize("contract", ["fast", "off"])
 @pytest.mark.parametrize("seed", [2025, 7])
-def test_filter_is_conservative(contract, seed):
-    exe = build(contract)
+def test_filter_is_conservative(contract, seed, rcp):
+    exe = build(contract, rcp)
     r = subprocess.run([exe, "1500000", str(seed)], capture_output=True, text=True, timeout=300)
     print(r.stdout[-2000:])
     assert r.returncode == 0, r.stdout[-3000:]

@@ -16,17 +16,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
 
 
-@pytest.mark.parametrize("fold,rcp", [(1, 0), (1, 1), (0, 0)])
+@pytest.mark.parametrize("fold,rcp", [(1, 0), (1, 1), (0, 0), (1, "2up"), (1, "2down")])
 @pytest.mark.parametrize("contract", ["fast", "off"])
 @pytest.mark.parametrize("seed", [2025, 7])
 def test_slab_is_conservative(contract, seed, fold, rcp):
     """fold = 1: the kernel's default (widening folded into the ray, RT_SLAB_FOLD);
     0: the widening applied per test.  rcp = 1: 1/d as an f32 quotient of d
-    rounded to f32 (RT_RCP_F32) instead of the f64 quotient rounded once."""
+    rounded to f32 (RT_RCP_F32) instead of the f64 quotient rounded once;
+    2up / 2down: the hardware reciprocal (RT_RCP_F32 = 2, v_rcp_f32, within an
+    ulp), emulated as the quotient moved one ulp up / down."""
     os.makedirs(BUILD, exist_ok=True)
-    exe = os.path.join(BUILD, "slab_prop_%s_%d_%d.%d" % (contract, fold, rcp, os.getpid()))  # one per pytest worker
+    exe = os.path.join(BUILD, "slab_prop_%s_%d_%s.%d" % (contract, fold, rcp, os.getpid()))  # one per pytest worker
     flags = ["-mfma", "-ffp-contract=fast"] if contract == "fast" else ["-ffp-contract=off"]
-    flags += ["-DRT_SLAB_FOLD=%d" % fold, "-DRT_RCP_F32=%d" % rcp]
+    if str(rcp).startswith("2"):
+        flags += ["-DRT_SLAB_FOLD=%d" % fold, "-DRT_RCP_F32=2", "-DRT_RCP_EMU=%d" % (1 if rcp == "2up" else -1)]
+    else:
+        flags += ["-DRT_SLAB_FOLD=%d" % fold, "-DRT_RCP_F32=%d" % rcp]
     subprocess.run(["g++", "-O2", "-std=c++17", *flags, os.path.join(HERE, "cpp", "slab_prop.cpp"), "-o", exe],
                    check=True)
     r = subprocess.run([exe, "1500000", str(seed)], capture_output=True, text=True, timeout=300)
