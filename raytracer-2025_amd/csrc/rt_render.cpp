@@ -123,6 +123,14 @@ struct DeviceWorld {
     size_t srgb_bytes = 0;
     void* stack_ovf = nullptr;  // mesh / full tiers: traversal-stack entries beyond the LDS part
     size_t stack_ovf_bytes = 0;
+    // the full tier's wavefront variant (RT_WAVEFRONT=1; rtk_launch_frame_wf):
+    // path slots in HBM and the walk kernel's grid
+    double* wf_d = nullptr;
+    uint32_t* wf_u = nullptr;
+    uint32_t* wf_ctr = nullptr;
+    size_t wf_slots = 0;
+    int wf_grid = 0;
+    bool wf_ok = false;
     hipStream_t own_stream = nullptr;  // for parts that do not run on the caller's stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     hipEvent_t ev_done = nullptr;  // after the slot's last device work (orders the next render)
@@ -173,6 +181,9 @@ static void destroy_device_world(DeviceWorld* d) {
     if (d->out) (void)hipFree(d->out);
     if (d->stack_ovf) (void)hipFree(d->stack_ovf);
     if (d->srgb) (void)hipFree(d->srgb);
+    if (d->wf_d) (void)hipFree(d->wf_d);
+    if (d->wf_u) (void)hipFree(d->wf_u);
+    if (d->wf_ctr) (void)hipFree(d->wf_ctr);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
     if (d->ev_done) (void)hipEventDestroy(d->ev_done);
@@ -301,6 +312,7 @@ struct FlatWorld {
     double ms = 0;
     int tier = 1;
     uint32_t stack_need = 0;
+    bool wf_ok = false;  // the full tier's wavefront variant may run this world (media fit its queue, one-pass)
     std::vector<char> blob;
     rtk::SceneView rel{};  // SceneView with byte offsets into blob instead of pointers
     size_t n_prims = 0;
@@ -391,6 +403,11 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.n_ref[rtk::K_POPXF] = 1;  // the marker's index is 0
     fw.tier = tier;
     fw.stack_need = hw.stack_need;
+    // the wavefront walk only queues media (no medium code in it): every
+    // medium must fit the queue (a walk meets each at most once) and have a
+    // one-pass boundary (rt_wf_shade tests them with boundary_onepass)
+    fw.wf_ok = tier == rtk::TIER_FULL && hw.media.size() <= RT_MEDIA_CAP;
+    for (const rtk::DMedium& m : hw.media) fw.wf_ok = fw.wf_ok && (m.planar_n || m.bsphere);
     fw.n_prims = hw.n_prims;
     fw.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
@@ -432,6 +449,11 @@ static int32_t slot_for(RenderState* r, size_t k, int device, DeviceWorld*& out)
         if (bpc < 1) bpc = 1;
         d->grid[t] = bpc * prop.multiProcessorCount;
     }
+    {
+        int bpc = 0;
+        if ((e = (hipError_t)rtk_wf_walk_occupancy(&bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
+        d->wf_grid = (bpc < 1 ? 1 : bpc) * prop.multiProcessorCount;
+    }
     d->cus = prop.multiProcessorCount;
     out = d;
     return RT_OK;
@@ -451,7 +473,9 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     hipError_t e;
     const uint32_t lds_entries = rtk::lds_stack_entries(fw.tier);
     if (fw.stack_need > lds_entries) {
-        const size_t need = (size_t)(fw.stack_need - lds_entries) * d->grid[fw.tier] * RT_BLOCK * sizeof(uint64_t);
+        // (the full tier's wavefront walk may run more blocks than its megakernel)
+        const int blocks = fw.tier == rtk::TIER_FULL ? std::max(d->grid[fw.tier], d->wf_grid) : d->grid[fw.tier];
+        const size_t need = (size_t)(fw.stack_need - lds_entries) * blocks * RT_BLOCK * sizeof(uint64_t);
         if (need > d->stack_ovf_bytes) {
             if (d->stack_ovf) (void)hipFree(d->stack_ovf);
             d->stack_ovf = nullptr;
@@ -477,6 +501,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
         fix(v.texels), fix(v.perlin);
     d->view = v;
     d->tier = fw.tier;
+    d->wf_ok = fw.wf_ok;
     d->reference_bvh = reference_bvh;
     d->blob_bytes = fw.blob.size();
     d->world = world;
@@ -656,7 +681,26 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     float* out = p.out ? p.out : d->out;
     p.out_used = out;
     const bool run = f.rows > 0 && f.max_depth > 0;
-    if (run) {
+    // RT_WAVEFRONT=1: the full tier's frame as wavefront bounces over
+    // RT_WF_SLOTS path slots (rt_kernel.hip rt_wf_walk / rt_wf_shade; A/B)
+    const bool wavefront = d->tier == rtk::TIER_FULL && d->wf_ok && env_u32("RT_WAVEFRONT", 0) == 1;
+    if (run && wavefront) {
+        const size_t n = env_u32("RT_WF_SLOTS", 1u << 21);
+        if (n > d->wf_slots) {
+            if (d->wf_d) (void)hipFree(d->wf_d);
+            if (d->wf_u) (void)hipFree(d->wf_u);
+            d->wf_d = nullptr, d->wf_u = nullptr, d->wf_slots = 0;
+            if ((e = hipMalloc(&d->wf_d, n * 17 * sizeof(double))) != hipSuccess) return fail(hip_fail(e, "hipMalloc wavefront slots"));
+            if ((e = hipMalloc(&d->wf_u, n * 19 * sizeof(uint32_t))) != hipSuccess)
+                return fail(hip_fail(e, "hipMalloc wavefront slots"));
+            d->wf_slots = n;
+        }
+        if (!d->wf_ctr && (e = hipMalloc(&d->wf_ctr, 256)) != hipSuccess) return fail(hip_fail(e, "hipMalloc wavefront counters"));
+        e = rtk_launch_frame_wf(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, p.stream, d->tier,
+                                d->wf_grid, d->params, d->stack_ovf, d->wf_d, d->wf_u, d->wf_ctr, (uint32_t)n,
+                                env_u32("RT_WF_CHECK", 32));
+        if (e != hipSuccess) return fail(hip_fail(e, "wavefront launch"));
+    } else if (run) {
         e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, p.stream, d->tier,
                              d->grid[d->tier], d->params, d->stack_ovf);
         if (e != hipSuccess) return fail(hip_fail(e, "kernel launch"));

@@ -4,7 +4,8 @@ by `make -C raytracer-2025_amd ab`) in one process on the C2 scene: each
 variant renders the same frame; path-kernel time from the library's HIP
 events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]; a variant is a library
 name (librt_ab_<name>.so) optionally followed by @VAR=val,... (environment
-variables set while its world is flattened, e.g. base@RT_SOME_KNOB=0).
+variables set while its world is flattened and its frames render, e.g.
+base@RT_WAVEFRONT=1).
 AB_WORKLOAD=c3|c4|c5 renders that config's scene (C5 at 1920 wide) instead of C2."""
 import ctypes
 import glob
@@ -64,7 +65,15 @@ res = {n: [] for n in names}
 for _ in range(reps):
     for n in names:
         scene, world, lights, cam, ref = runs[n]
+        env = dict(kv.split("=", 1) for kv in n.partition("@")[2].split(",") if kv)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)  # (knobs read per render, e.g. RT_WAVEFRONT)
         lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         res[n].append(st.kernel_ms)
         print(n, st.kernel_ms, file=sys.stderr, flush=True)
 base = runs[names[0]][4]

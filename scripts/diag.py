@@ -37,7 +37,7 @@ elif wl == "c5":
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 24)()
 lib.rt_diag_counters(buf, 1)
 _, _, st = cam.render(world, lights, seed=1, want_srgb=False)
 lib.rt_diag_counters(buf, 0)
@@ -60,6 +60,13 @@ out = {
     "pops_per_ray": c[11] / c[8],
     "big_sphere_exact_tests_per_ray": c[14] / c[8],  # basic tier: spheres with r > 100 (C2's ground)
     "big_sphere_exact_hits_per_ray": c[15] / c[8],
-    "raw": c[:16],
+    # mesh / full tiers: unified walk-step loads -- wave steps whose active
+    # lanes all read one record (a scalar load could serve them), of them node
+    # records, and the mean share of active lanes on the first lane's record
+    "uniform_step_share": c[17] / c[16] if c[16] else None,
+    "uniform_node_step_share": c[18] / c[16] if c[16] else None,
+    "lanes_on_first_record": c[20] / c[19] if c[19] else None,
+    "active_lanes_per_step": c[19] / c[16] if c[16] else None,
+    "raw": c[:24],
 }
 print(json.dumps(out, indent=1))
