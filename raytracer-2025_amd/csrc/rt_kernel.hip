@@ -390,9 +390,16 @@ __device__ __forceinline__ D3 quat_rotate(double w, double x, double y, double z
               ((pw * cz + px * cy) - py * cx) + pz * w);
 }
 // Transform::detransform (shapes.rs:80-84): conj(q).rotate_vector(v - offset) / scale
+#ifndef RT_XF_UNIT
+// 1: a Transform whose scale is exactly (1, 1, 1) (the reference's `None`,
+// every Transform of C3 and C5) skips the three f64 divisions: x / 1.0 is x,
+// bit for bit, NaN, infinities and signed zeros included
+#define RT_XF_UNIT 1
+#endif
 __device__ __forceinline__ D3 xf_in(const DXform& X, D3 v) {
-    return quat_rotate(X.q[0], -X.q[1], -X.q[2], -X.q[3], v - d3(X.off[0], X.off[1], X.off[2])) /
-           d3(X.scale[0], X.scale[1], X.scale[2]);
+    const D3 p = quat_rotate(X.q[0], -X.q[1], -X.q[2], -X.q[3], v - d3(X.off[0], X.off[1], X.off[2]));
+    if (RT_XF_UNIT && (X.flags & XF_UNIT_SCALE)) return p;
+    return p / d3(X.scale[0], X.scale[1], X.scale[2]);
 }
 // Transform::transform (shapes.rs:74-78): q.rotate_vector(v * scale) + offset
 __device__ __forceinline__ D3 xf_out(const DXform& X, D3 v) {
@@ -999,13 +1006,29 @@ struct RayLds {
 __device__ __forceinline__ RayReg world_ray(const Ray& r) { return RayReg{r}; }
 __device__ __forceinline__ const RayLds& world_ray(const RayLds& r) { return r; }
 
+// A lane's media queue (full tiers) in the lane rows of the LDS arena:
+// entry k = {medium, nxf, xf a, xf b} in rows 2k and 2k + 1 (uint2, RT_BLOCK
+// apart), so that it shares the one per-lane base address of the stack and
+// the parked path state (rt_path_kernel's lane arena)
+struct MedQ {
+    RT_LDS uint2* p;
+    __device__ __forceinline__ void set(uint32_t k, uint4 v) const {
+        p[(2 * k) * RT_BLOCK] = make_uint2(v.x, v.y);
+        p[(2 * k + 1) * RT_BLOCK] = make_uint2(v.z, v.w);
+    }
+    __device__ __forceinline__ uint4 get(uint32_t k) const {
+        const uint2 a = p[(2 * k) * RT_BLOCK], b = p[(2 * k + 1) * RT_BLOCK];
+        return make_uint4(a.x, a.y, b.x, b.y);
+    }
+};
+
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
 // INLINE_MEDIA false (the wavefront walk): a medium is only ever queued --
 // the world's media fit the queue (rt_render.cpp) -- and a full queue is
 // counted as a panic rather than tested here.
 template <int TIER, class WR, bool INLINE_MEDIA = true>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                           const Rng& rng, RT_LDS uint4* med, Diag& dg, uint32_t* overflow = nullptr) {
+                                           const Rng& rng, MedQ med, Diag& dg, uint32_t* overflow = nullptr) {
     const auto wq = world_ray(wrr);
     constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
@@ -1066,7 +1089,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                 // step of its own and the pop of the rest of the list
                 const bool queue = RT_FLAT_MEDIA_IN_LIST && in_box && ck == K_MEDIUM && T.nmed < RT_MEDIA_CAP;
                 if (queue) {
-                    med[T.nmed * RT_BLOCK] = make_uint4(ref_idx(S, child), T.nxf, T.xfs.a, T.xfs.b);
+                    med.set(T.nmed, make_uint4(ref_idx(S, child), T.nxf, T.xfs.a, T.xfs.b));
                     ++T.nmed;
                 }
                 if (!in_box || queue) {
@@ -1193,7 +1216,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                 // walk against the walk's closest t (media_phase); only a
                 // lane whose queue is full tests it here.
                 if (T.nmed < RT_MEDIA_CAP) {
-                    med[T.nmed * RT_BLOCK] = make_uint4(idx, T.nxf, T.xfs.a, T.xfs.b);
+                    med.set(T.nmed, make_uint4(idx, T.nxf, T.xfs.a, T.xfs.b));
                     ++T.nmed;
                 } else if constexpr (INLINE_MEDIA) {
                     got = medium_hit<TIER != TIER_FULL_FLAT>(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
@@ -1217,10 +1240,10 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
 // against the walk's closest t; the walk's stack is free again.
 template <int TIER, class WR>
 __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                            const Rng& rng, const RT_LDS uint4* med) {
+                                            const Rng& rng, MedQ med) {
     const auto wq = world_ray(wrr);
     for (uint32_t k = 0; k < T.nmed; ++k) {
-        const uint4 e = med[k * RT_BLOCK];
+        const uint4 e = med.get(k);
         Ray r = wq.get();
         for (uint32_t j = 0; j < e.y; ++j) r = xf_ray(S.xforms[j == 0 ? e.z : e.w], r);
         double t;
@@ -2116,14 +2139,25 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     constexpr int STACK = lds_stack_entries(TIER);
     constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
     constexpr bool B4 = TIER == TIER_BASIC && RT_STACK4B;
-    __shared__ uint2 stack_lds[B4 ? 1 : STACK * BLK];
+    // The lane arena (all tiers but the basic one): one uint2 row per lane and
+    // row, RT_BLOCK apart -- the stack's rows, then (full tiers) the media
+    // queue's (MedQ), then (full-flat tier) the parked path state's -- so
+    // that every per-lane LDS access is one base address (threadIdx.x * 8)
+    // plus a constant in the instruction's offset field, not a base VGPR per
+    // array held across the path loop
+    constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
+    constexpr bool PARK_RAY = LDS_STATE && RT_FLAT_PARK_RAY;  // + the world ray (7 doubles)
+    constexpr uint32_t R_MED = B4 ? 0u : (uint32_t)STACK;
+    constexpr uint32_t R_PST = R_MED + (tier_full(TIER) ? 2u * RT_MEDIA_CAP : 0u);
+    constexpr uint32_t R_PIT = R_PST + (LDS_STATE ? (PARK_RAY ? 16u : 9u) : 0u);
+    constexpr uint32_t R_END = R_PIT + (LDS_STATE ? 2u : 0u);
+    __shared__ uint2 lane_lds[B4 ? 1 : R_END * BLK];
     __shared__ uint32_t stack4_lds[B4 ? STACK * BLK : 1];
-    __shared__ uint4 media_lds[tier_full(TIER) && RT_MEDIA_CAP > 0 ? RT_MEDIA_CAP * RT_BLOCK : 1];
-    RT_LDS uint4* med = (RT_LDS uint4*)(media_lds + threadIdx.x);
+    RT_LDS uint2* const lrow = (RT_LDS uint2*)(lane_lds + threadIdx.x);
+    const MedQ med{lrow + R_MED * BLK};
     __shared__ uint16_t pend_lds[TIER == TIER_BASIC && RT_BVH4 ? RT_PEND_CAP * BLK : 1];
     RT_LDS uint16_t* pq = (RT_LDS uint16_t*)(pend_lds + threadIdx.x);
-    StackFor<TIER> stk = make_stack<TIER>((RT_LDS uint2*)(stack_lds + threadIdx.x),
-                                          (RT_LDS uint32_t*)(stack4_lds + threadIdx.x),
+    StackFor<TIER> stk = make_stack<TIER>(lrow, (RT_LDS uint32_t*)(stack4_lds + threadIdx.x),
                                           P->stack_ovf + (uint64_t)blockIdx.x * BLK + threadIdx.x, gridDim.x * BLK);
     // Basic tier with shading batches: the walk state of a lane whose walk
     // carries over a shading round is parked here across it (RT_PARK_WORDS
@@ -2159,16 +2193,15 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             __syncthreads();
         }
     }
-    const uint32_t lane = __lane_id();
     // Full-flat tier: the path state the walk never reads (beta, L, acc, the
     // item's fields) is parked in LDS across the walk, so that its registers
     // are free there instead of spilled to scratch around it.
-    constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
-    constexpr bool PARK_RAY = LDS_STATE && RT_FLAT_PARK_RAY;  // + the world ray (7 doubles)
-    __shared__ double pstate_lds[LDS_STATE ? (PARK_RAY ? 16 : 9) * RT_BLOCK : 1];
-    __shared__ uint4 pitem_lds[LDS_STATE ? RT_BLOCK : 1];
-    RT_LDS double* pst = (RT_LDS double*)(pstate_lds + threadIdx.x);
-    RT_LDS uint4* pit = (RT_LDS uint4*)(pitem_lds + threadIdx.x);
+    RT_LDS double* const pst = (RT_LDS double*)(lrow + R_PST * BLK);
+    RT_LDS uint2* const pit = lrow + R_PIT * BLK;
+    // ... and the queue entry's running sum and part-sum slot stay there for
+    // the whole entry (pst rows 6-8, pit row 1 .y): read at the sample's end
+    // only, they hold no registers through the shading code
+    constexpr bool ACC_LDS = LDS_STATE;
 
     Rng rng;
     rng.k0 = F.key0;
@@ -2236,11 +2269,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
             }
 #endif
+            // the lane's rank among the needy lanes (the leader: rank 0 with
+            // need); the leader's atomic result is read with v_readlane -- no
+            // lane id held across the loop, no ds_bpermute
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             if (avail < n) {
                 if (!dry) {
                     const uint32_t leader = __ffsll((long long)mask) - 1;
-                    if (lane == leader) fresh = atomicAdd(queue, chunk);
-                    fresh = __shfl(fresh, leader) + F.static_entries;
+                    if (need && rank == 0) fresh = atomicAdd(queue, chunk);
+                    fresh = __builtin_amdgcn_readlane(fresh, leader) + F.static_entries;
                     dry = fresh + chunk >= F.queue_total;
                 } else {
                     fresh = F.queue_total;  // past the end: the needy lanes leave
@@ -2254,8 +2292,6 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pool_next += n;
             }
             if (need) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
                 const uint32_t q = rank < avail ? old_next + rank : fresh + (rank - avail);
                 if (q >= F.queue_total) return false;
                 need = false;
@@ -2444,11 +2480,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
             }
 #endif
+            // the lane's rank among the needy lanes (the leader: rank 0 with
+            // need); the leader's atomic result is read with v_readlane -- no
+            // lane id held across the loop, no ds_bpermute
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             if (avail < n) {
                 if (!dry) {
                     const uint32_t leader = __ffsll((long long)mask) - 1;
-                    if (lane == leader) fresh = atomicAdd(queue, chunk);
-                    fresh = __shfl(fresh, leader) + F.static_entries;
+                    if (need && rank == 0) fresh = atomicAdd(queue, chunk);
+                    fresh = __builtin_amdgcn_readlane(fresh, leader) + F.static_entries;
                     dry = fresh + chunk >= F.queue_total;
                 } else {
                     fresh = F.queue_total;  // past the end: the needy lanes leave
@@ -2462,8 +2503,6 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 pool_next += n;
             }
             if (need) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
                 const uint32_t q = rank < avail ? old_next + rank : fresh + (rank - avail);
                 if (q >= F.queue_total) break;
                 need = false;
@@ -2479,10 +2518,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
                 const uint32_t item = whole ? q : F.whole_items + it;
                 s_j = whole ? 0u : part * F.part_len;
-                acc = d3(0, 0, 0);
+                if constexpr (ACC_LDS)  // the entry's sum lives in LDS (flat tier)
+                    pst[6 * RT_BLOCK] = 0.0, pst[7 * RT_BLOCK] = 0.0, pst[8 * RT_BLOCK] = 0.0;
+                else
+                    acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
                 sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
-                slot = q;
+                if constexpr (ACC_LDS)
+                    pit[BLK].y = q;
+                else
+                    slot = q;
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
             }
@@ -2550,8 +2595,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if constexpr (LDS_STATE) {
                 pst[0 * RT_BLOCK] = beta.x, pst[1 * RT_BLOCK] = beta.y, pst[2 * RT_BLOCK] = beta.z;
                 pst[3 * RT_BLOCK] = L.x, pst[4 * RT_BLOCK] = L.y, pst[5 * RT_BLOCK] = L.z;
-                pst[6 * RT_BLOCK] = acc.x, pst[7 * RT_BLOCK] = acc.y, pst[8 * RT_BLOCK] = acc.z;
-                *pit = make_uint4(slot, sie, s_j, 0u);
+                pit[0] = make_uint2(sie, s_j);
                 if constexpr (PARK_RAY) {
                     pst[9 * RT_BLOCK] = ray.o.x, pst[10 * RT_BLOCK] = ray.o.y, pst[11 * RT_BLOCK] = ray.o.z;
                     pst[12 * RT_BLOCK] = ray.d.x, pst[13 * RT_BLOCK] = ray.d.y, pst[14 * RT_BLOCK] = ray.d.z;
@@ -2573,9 +2617,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 if constexpr (PARK_RAY) ray = RayLds{pst + 9 * RT_BLOCK}.get();
                 beta = d3(pst[0 * RT_BLOCK], pst[1 * RT_BLOCK], pst[2 * RT_BLOCK]);
                 L = d3(pst[3 * RT_BLOCK], pst[4 * RT_BLOCK], pst[5 * RT_BLOCK]);
-                acc = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]);
-                const uint4 it = *pit;
-                slot = it.x, sie = it.y, s_j = it.z;
+                const uint2 it = pit[0];
+                sie = it.x, s_j = it.y;
             }
         } else {
             const unsigned long long active = __ballot(true);
@@ -2618,19 +2661,33 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 ++n_panics;
                 L = d3(0, 0, 0);
             }
-            acc = acc + L;
             in_path = false;
             ++s_j;
-            if (s_j == (sie >> 16)) {
-                double* dst = P->partial + (uint64_t)slot * 3;
-                dst[0] = acc.x;
-                dst[1] = acc.y;
-                dst[2] = acc.z;
-                need = true;
+            if constexpr (ACC_LDS) {
+                const D3 a = d3(pst[6 * RT_BLOCK], pst[7 * RT_BLOCK], pst[8 * RT_BLOCK]) + L;
+                if (s_j == (sie >> 16)) {
+                    double* dst = P->partial + (uint64_t)pit[BLK].y * 3;
+                    dst[0] = a.x;
+                    dst[1] = a.y;
+                    dst[2] = a.z;
+                    need = true;
+                } else {
+                    pst[6 * RT_BLOCK] = a.x, pst[7 * RT_BLOCK] = a.y, pst[8 * RT_BLOCK] = a.z;
+                }
+            } else {
+                acc = acc + L;
+                if (s_j == (sie >> 16)) {
+                    double* dst = P->partial + (uint64_t)slot * 3;
+                    dst[0] = acc.x;
+                    dst[1] = acc.y;
+                    dst[2] = acc.z;
+                    need = true;
+                }
             }
         }
     }
     }  // full tiers
+    const uint32_t lane = __lane_id();
 #ifdef RT_DIAG
     // wave-uniform cycle counts: lane 0 of each wave; lane counters: every lane
     if (lane == 0) {
@@ -2741,10 +2798,10 @@ __global__ void __launch_bounds__(RT_BLOCK, RT_WF_WALK_WAVES) rt_wf_walk(const W
     const WfSlots W = P->W;
     const size_t n = W.n;
     constexpr int STACK = lds_stack_entries(TIER);
-    __shared__ uint2 stack_lds[STACK * RT_BLOCK];
-    __shared__ uint4 media_lds[RT_MEDIA_CAP * RT_BLOCK];
-    RT_LDS uint4* med = (RT_LDS uint4*)(media_lds + threadIdx.x);
-    StackFor<TIER> stk = make_stack<TIER>((RT_LDS uint2*)(stack_lds + threadIdx.x), (RT_LDS uint32_t*)(stack_lds + threadIdx.x),
+    __shared__ uint2 lane_lds[(STACK + 2 * RT_MEDIA_CAP) * RT_BLOCK];  // stack rows, then MedQ's
+    RT_LDS uint2* const lrow = (RT_LDS uint2*)(lane_lds + threadIdx.x);
+    const MedQ med{lrow + STACK * RT_BLOCK};
+    StackFor<TIER> stk = make_stack<TIER>(lrow, (RT_LDS uint32_t*)lrow,
                                           P->K.stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x,
                                           gridDim.x * RT_BLOCK);
     const uint32_t lane = __lane_id();
@@ -2804,7 +2861,7 @@ __global__ void __launch_bounds__(RT_BLOCK, RT_WF_WALK_WAVES) rt_wf_walk(const W
             W.u[9 * n + slot] = T.hit.xf.b;
             W.u[10 * n + slot] = T.nmed;
             for (uint32_t k = 0; k < T.nmed; ++k) {
-                const uint4 e = med[k * RT_BLOCK];
+                const uint4 e = med.get(k);
                 uint32_t* m = W.u + (11 + 4 * k) * n + slot;
                 m[0] = e.x, m[n] = e.y, m[2 * n] = e.z, m[3 * n] = e.w;
             }

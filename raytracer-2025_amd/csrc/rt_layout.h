@@ -131,8 +131,10 @@ struct alignas(16) DXform {
     double off[3];
     double scale[3];
     double q[4];  // w, x, y, z
-    uint32_t child, pad;
+    uint32_t child;
+    uint32_t flags;  // XF_UNIT_SCALE: scale is exactly (1, 1, 1)
 };
+constexpr uint32_t XF_UNIT_SCALE = 1;
 
 constexpr uint32_t RT_MED_PLANAR_MAX = 6;  // elements of a one-pass medium boundary (build_box: 6)
 

@@ -772,6 +772,7 @@ struct Flattener {
                 x.q[2] = o.q.y;
                 x.q[3] = o.q.z;
                 x.child = C.first;
+                x.flags = (o.scale.x == 1.0 && o.scale.y == 1.0 && o.scale.z == 1.0) ? rtk::XF_UNIT_SCALE : 0u;
                 out.xforms.push_back(x);
                 out.features |= rtk::F_XFORM;
                 r = {rtk::make_ref(rtk::K_XFORM, idx), 1 + C.second};
