@@ -34,7 +34,7 @@ def main():
     world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
     cam.render(world, lights, seed=1, want_srgb=False)  # flatten + upload
     base_env = dict(os.environ)
-    res = {k: {"full": [], "worst8": []} for k in settings}
+    res = {k: {"full": [], "worst8": [], "sum8": []} for k in settings}
     ref = None
     for rep in range(reps):
         for k in settings:
@@ -46,20 +46,27 @@ def main():
                 ref = lin
             rel = float(abs(lin.astype("float64") - ref).max())  # settings may change f64 sum order: ~1 ulp
             res[k]["full"].append(st.kernel_ms)
-            worst = 0.0
+            shards = []
             for r in range(8):
                 _, _, st8 = cam.render(world, lights, seed=1, row_offset=r, row_stride=8, want_srgb=False)
-                worst = max(worst, st8.kernel_ms)
+                shards.append(st8.kernel_ms)
+            worst = max(shards)
             res[k]["worst8"].append(worst)
+            res[k]["sum8"].append(sum(shards))
             print(json.dumps({"rep": rep, "setting": k, "full_ms": round(st.kernel_ms, 3),
-                              "worst8_ms": round(worst, 3), "max_abs_vs_first": rel}), flush=True)
+                              "worst8_ms": round(worst, 3), "shards_ms": [round(x, 3) for x in shards],
+                              "max_abs_vs_first": rel}), flush=True)
     os.environ.clear()
     os.environ.update(base_env)
     out = {}
     for k, v in res.items():
         out[k] = {"full_min": min(v["full"]), "full_median": statistics.median(v["full"]),
                   "worst8_min": min(v["worst8"]), "worst8_median": statistics.median(v["worst8"]),
-                  "eff8": min(v["full"]) / (8 * min(v["worst8"]))}
+                  "eff8": min(v["full"]) / (8 * min(v["worst8"])),
+                  # the shards' summed kernel time against the frame's: < 1
+                  # when a shard's samples cost more than the frame's (cache
+                  # locality, launch ramp and drain), apart from imbalance
+                  "sum8_over_full": min(v["sum8"]) / min(v["full"])}
     print(json.dumps({"workload": desc, "spp": spp, "reps": reps, "settings": out}))
 
 
