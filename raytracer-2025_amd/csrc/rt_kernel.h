@@ -95,6 +95,9 @@ struct rtk_frame_desc {
     uint32_t chunk_cap;  // most entries per queue atomic (0: the tier's RT_QUEUE_CHUNK[_MESH])
     uint32_t guide;      // guided chunks: work left / (waves x guide) (0: RT_QUEUE_GUIDE)
     uint32_t chunk_min_whole;  // smallest guided chunk while whole-row entries are left
+    // the shard's rows from fine_row on (the frame's last rtk_tail_split
+    // `fine` rows) go out in parts2 entries per stratum row
+    uint32_t parts2, fine_row;
 
     double recip_sqrt_spp, pixel_sample_scale;
     double center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3];
@@ -127,6 +130,14 @@ extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples);
 extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint64_t budget_bytes,
                                   uint32_t permille);
 // The rows of a shard (image rows row_offset + r * row_stride, r < rows) above
+// The frame's tail and, within it, its fine rows: the last `fine` image rows
+// (about fine_permille / 1000 of H, within half the budget and half the
+// queue's room) go out in parts2 entries per stratum row, the `tail` - `fine`
+// rows above them in `parts`; tail >= fine.  Like rtk_tail_rows a function
+// of the frame only.
+extern "C" void rtk_tail_split(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint32_t parts2,
+                               uint64_t budget_bytes, uint32_t permille, uint32_t fine_permille, uint32_t* tail,
+                               uint32_t* fine);
 // a frame's tail of `tail` rows: its first rtk_shard_whole_rows rows; the rest
 // are tail rows, each shard's last.
 extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row_offset, uint32_t row_stride,

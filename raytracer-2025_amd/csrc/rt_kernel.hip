@@ -95,19 +95,28 @@ struct Frame {
     // samples s_j (the last part the rest), so that the last entries of a
     // launch are short: a whole row of a pixel whose paths bounce 40 times
     // inside a glass sphere is ~10 ms of one wave (scripts/lane_trace.py).
+    // The frame's last `fine` rows (rtk_tail_split) go out in finer parts
+    // still -- parts2 entries of part_len2 samples, from queue entry fine_q0
+    // and item fine_item0 on -- so that what is in flight when the queue
+    // runs dry is about one sample a lane: a 1/8 row shard of C4 drained for
+    // ~3 ms after its last 4-sample part was handed out (lane_trace_c4.json).
     // Entry q writes its f64 sum to partial slot q (queue order: the lanes
     // of a wave take consecutive entries, so their 24-B sums fill whole L2
     // lines), and the reduce adds a tail row's parts in part order.
     uint32_t parts, part_len, queue_total, whole_items;
+    uint32_t parts2, part_len2, fine_q0, fine_item0;
     uint32_t static_entries;  // 64 per wave of the grid: their first pools, taken without the counter
     uint32_t chunk_min;  // smallest guided chunk (queue entries per atomic)
     uint32_t chunk_cap;  // largest guided chunk
     uint32_t chunk_min_whole;  // smallest guided chunk while whole-row entries are left
     // 1/parts, 1/S, 1/W rounded up (udiv_inv), and 1/(waves of the grid x
     // RT_QUEUE_GUIDE): the queue-entry decode without integer divisions
-    double inv_parts, inv_S, inv_W;
+    double inv_parts, inv_parts2, inv_S, inv_W;
     float inv_guide;
-    float parts_m1, inv_parts_f;  // parts - 1 and 1 / parts: the guided chunk in part-sized entries
+    // samples per entry of each region and their reciprocals: the guided
+    // chunk is the work left in samples / (waves x guide), in the entries of
+    // the region the pool starts in
+    float S_f, part_len_f, part_len2_f, inv_S_f, inv_part_len_f, inv_part_len2_f;
     uint32_t defocus;
     double recip_sqrt_spp, pixel_sample_scale;
     D3 center, pixel00, du, dv, disk_u, disk_v;
@@ -2108,6 +2117,33 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 #define RT_MESH_WAVES 4  // beats 2 waves (164.7 vs 263.8 ms, C4 64 spp) and 3 / 5 waves (+16 % / +12 %)
 #endif
 
+// Queue entry q -> its stratum-row item and samples [s_j, s_end) (Frame:
+// whole rows, then parts, then the fine parts of the frame's last rows).
+__device__ __forceinline__ void queue_entry(const Frame& F, uint32_t q, uint32_t& item, uint32_t& s_j,
+                                            uint32_t& s_end) {
+    const bool whole = q < F.whole_items, fine = q >= F.fine_q0;
+    const uint32_t qt = whole ? 0u : q - (fine ? F.fine_q0 : F.whole_items);  // (udiv_inv wants n < 2^32 in range)
+    const uint32_t np = fine ? F.parts2 : F.parts, pl = fine ? F.part_len2 : F.part_len;
+    const uint32_t it = udiv_inv(qt, fine ? F.inv_parts2 : F.inv_parts), part = qt - it * np;
+    item = whole ? q : (fine ? F.fine_item0 : F.whole_items) + it;
+    s_j = whole ? 0u : part * pl;
+    s_end = whole ? F.S : min(F.S, s_j + pl);
+}
+// The guided chunk of a wave whose pool ends at pool_end: about 1/GUIDE of
+// the samples left (as last seen) per wave of the grid, in the entries of
+// the region the next pool starts in; never below what the wave's lanes need
+// now (n lanes, avail entries in the pool), nor below Frame::chunk_min.
+__device__ __forceinline__ uint32_t guided_chunk(const Frame& F, uint32_t pool_end, uint32_t avail, uint32_t n) {
+    const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
+    const uint32_t p0 = max(pool_end, F.whole_items), part_left = F.fine_q0 > p0 ? F.fine_q0 - p0 : 0u;
+    const uint32_t f0 = max(pool_end, F.fine_q0), fine_left = F.queue_total > f0 ? F.queue_total - f0 : 0u;
+    const float g = ((float)whole_left * F.S_f + (float)part_left * F.part_len_f + (float)fine_left * F.part_len2_f) *
+                    F.inv_guide;
+    const float inv_per = whole_left ? F.inv_S_f : (part_left ? F.inv_part_len_f : F.inv_part_len2_f);
+    const uint32_t chunk = min((uint32_t)(g * inv_per), F.chunk_cap);
+    return max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
+}
+
 // Launch parameters live in device memory and are read where they are used
 // (scalar loads), not pinned in SGPRs for the life of the kernel.
 struct KParams {
@@ -2255,20 +2291,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             // Frame::chunk_min.  Near the end a wave takes only what its lanes
             // need: a pool held by a slow wave (deep glass paths) is work the
             // idle waves cannot take (scripts/lane_trace.py).
-            uint32_t chunk = RT_QUEUE_CHUNK;
-#if RT_QUEUE_GUIDE
-            {
-                // the work left in part-sized entries (a whole-row entry is
-                // `parts` of them), and the chunk in the entries it takes: a
-                // pool of whole rows taken as the tail starts is no larger
-                // in samples than the tail's pools (it would outlast them)
-                const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
-                const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
-                const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
-                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), F.chunk_cap);
-                chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
-            }
-#endif
+            // (the chunk in the entries it takes: a pool of whole rows taken
+            // as the tail starts is no larger in samples than the tail's
+            // pools -- it would outlast them)
+            const uint32_t chunk = RT_QUEUE_GUIDE ? guided_chunk(F, pool_end, avail, n) : (uint32_t)RT_QUEUE_CHUNK;
             // the lane's rank among the needy lanes (the leader: rank 0 with
             // need); the leader's atomic result is read with v_readlane -- no
             // lane id held across the loop, no ds_bpermute
@@ -2302,14 +2328,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_steps_q = trace_steps;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                const bool whole = q < F.whole_items;
-                const uint32_t qt = whole ? 0u : q - F.whole_items;  // (udiv_inv wants n < 2^32 in range)
-                const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
-                const uint32_t item = whole ? q : F.whole_items + it;
-                s_j = whole ? 0u : part * F.part_len;
+                uint32_t item, s_end;
+                queue_entry(F, q, item, s_j, s_end);
                 acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
-                sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
+                sie = s_i | (s_end << 16);
                 slot = q;
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
@@ -2466,20 +2489,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             // Frame::chunk_min.  Near the end a wave takes only what its lanes
             // need: a pool held by a slow wave (deep glass paths) is work the
             // idle waves cannot take (scripts/lane_trace.py).
-            uint32_t chunk = RT_QUEUE_CHUNK;
-#if RT_QUEUE_GUIDE
-            {
-                // the work left in part-sized entries (a whole-row entry is
-                // `parts` of them), and the chunk in the entries it takes: a
-                // pool of whole rows taken as the tail starts is no larger
-                // in samples than the tail's pools (it would outlast them)
-                const uint32_t left = F.queue_total > pool_end ? F.queue_total - pool_end : 0u;
-                const uint32_t whole_left = F.whole_items > pool_end ? F.whole_items - pool_end : 0u;
-                const float g = ((float)left + (float)whole_left * F.parts_m1) * F.inv_guide;
-                chunk = min((uint32_t)(whole_left ? g * F.inv_parts_f : g), F.chunk_cap);
-                chunk = max(max(chunk, whole_left ? F.chunk_min_whole : F.chunk_min), avail < n ? n - avail : 0u);
-            }
-#endif
+            // (the chunk in the entries it takes: a pool of whole rows taken
+            // as the tail starts is no larger in samples than the tail's
+            // pools -- it would outlast them)
+            const uint32_t chunk = RT_QUEUE_GUIDE ? guided_chunk(F, pool_end, avail, n) : (uint32_t)RT_QUEUE_CHUNK;
             // the lane's rank among the needy lanes (the leader: rank 0 with
             // need); the leader's atomic result is read with v_readlane -- no
             // lane id held across the loop, no ds_bpermute
@@ -2513,17 +2526,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 trace_steps_q = trace_steps;
                 trace_tq = __builtin_amdgcn_s_memrealtime();
 #endif
-                const bool whole = q < F.whole_items;
-                const uint32_t qt = whole ? 0u : q - F.whole_items;  // (udiv_inv wants n < 2^32 in range)
-                const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
-                const uint32_t item = whole ? q : F.whole_items + it;
-                s_j = whole ? 0u : part * F.part_len;
+                uint32_t item, s_end;
+                queue_entry(F, q, item, s_j, s_end);
                 if constexpr (ACC_LDS)  // the entry's sum lives in LDS (flat tier)
                     pst[6 * RT_BLOCK] = 0.0, pst[7 * RT_BLOCK] = 0.0, pst[8 * RT_BLOCK] = 0.0;
                 else
                     acc = d3(0, 0, 0);
                 const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
-                sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
+                sie = s_i | (s_end << 16);
                 if constexpr (ACC_LDS)
                     pit[BLK].y = q;
                 else
@@ -2987,13 +2997,10 @@ __global__ void __launch_bounds__(RT_BLOCK, RT_WF_SHADE_WAVES) rt_wf_shade(const
                 fl = 0u;  // no more work for this slot
             } else {
                 fl &= ~WF_NEED;
-                const bool whole = q < F.whole_items;
-                const uint32_t qt = whole ? 0u : q - F.whole_items;
-                const uint32_t it = udiv_inv(qt, F.inv_parts), part = qt - it * F.parts;
-                const uint32_t item = whole ? q : F.whole_items + it;
-                s_j = whole ? 0u : part * F.part_len;
+                uint32_t item, s_end;
+                queue_entry(F, q, item, s_j, s_end);
                 const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
-                sie = s_i | ((whole ? F.S : min(F.S, s_j + F.part_len)) << 16);
+                sie = s_i | (s_end << 16);
                 const uint32_t prow = udiv_inv(pl, F.inv_W);
                 rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
                 double* a = W.d + 13 * n + slot;
@@ -3171,15 +3178,21 @@ __device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
 // lines per load, three times: 1.8 ms for C2's 3.8 GB against 0.8 at HBM rate).
 constexpr uint32_t REDUCE_PX_PER_WAVE = 21;
 __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
-                                                       uint32_t parts, uint32_t whole_px, double scale,
-                                                       float* __restrict__ out, uint8_t* __restrict__ srgb, int toon) {
+                                                       uint32_t parts, uint32_t whole_px, uint32_t parts2,
+                                                       uint32_t fine_px, double scale, float* __restrict__ out,
+                                                       uint8_t* __restrict__ srgb, int toon) {
     const uint32_t lane = threadIdx.x & 63u, wave = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
     if (lane >= 3u * REDUCE_PX_PER_WAVE) return;
     const uint32_t p = wave * REDUCE_PX_PER_WAVE + lane / 3u, c = lane % 3u;
     if (p >= npix) return;
-    const bool whole = p < whole_px;
-    const uint32_t np = whole ? 1u : parts;
-    const uint64_t first = whole ? (uint64_t)p * S : (uint64_t)whole_px * S + (uint64_t)(p - whole_px) * S * parts;
+    // pixels [0, whole_px): one sum per stratum row; [whole_px, fine_px):
+    // `parts`; [fine_px, npix): `parts2` (the fine rows)
+    const bool whole = p < whole_px, fine = p >= fine_px;
+    const uint32_t np = whole ? 1u : (fine ? parts2 : parts);
+    const uint64_t part_first = (uint64_t)whole_px * S + (uint64_t)(fine_px - whole_px) * S * parts;
+    const uint64_t first = whole ? (uint64_t)p * S
+                         : fine  ? part_first + (uint64_t)(p - fine_px) * S * parts2
+                                 : (uint64_t)whole_px * S + (uint64_t)(p - whole_px) * S * parts;
     const double* src = partial + first * 3 + c;
     double acc = 0.0;
     for (uint32_t k = 0; k < S; ++k) {
@@ -3299,16 +3312,27 @@ static void fill_kparams(rtk::KParams& K, const rtk::SceneView* view, const rtk_
     F.total_items = fd->W * fd->rows * fd->S;
     F.parts = fd->parts > 1 ? fd->parts : 1u;  // the host's rtk_row_parts: no part empty
     F.part_len = (fd->S + F.parts - 1) / F.parts;
-    const uint32_t whole_rows = fd->whole_rows < fd->rows ? fd->whole_rows : fd->rows;
-    F.whole_items = F.parts > 1 ? fd->W * whole_rows * fd->S : F.total_items;
-    F.queue_total = F.whole_items + (F.total_items - F.whole_items) * F.parts;
+    F.parts2 = fd->parts2 > 1 ? fd->parts2 : F.parts;
+    F.part_len2 = (fd->S + F.parts2 - 1) / F.parts2;
+    const uint32_t whole_rows = F.parts > 1 ? (fd->whole_rows < fd->rows ? fd->whole_rows : fd->rows) : fd->rows;
+    // the shard's rows from fine_row on are the fine rows (none: rows)
+    const uint32_t fine_row = fd->fine_row < whole_rows ? whole_rows : (fd->fine_row < fd->rows ? fd->fine_row : fd->rows);
+    F.whole_items = fd->W * whole_rows * fd->S;
+    F.fine_item0 = fd->W * fine_row * fd->S;
+    F.fine_q0 = F.whole_items + (F.fine_item0 - F.whole_items) * F.parts;
+    F.queue_total = F.fine_q0 + (F.total_items - F.fine_item0) * F.parts2;
     F.static_entries = static_entries;
     F.chunk_min = fd->chunk_min;
     F.chunk_min_whole = fd->chunk_min_whole;
     auto inv_up = [](uint32_t d) { return std::nextafter(1.0 / (double)d, 2.0); };
     F.inv_parts = inv_up(F.parts);
-    F.parts_m1 = (float)(F.parts - 1);
-    F.inv_parts_f = 1.0f / (float)F.parts;
+    F.inv_parts2 = inv_up(F.parts2);
+    F.S_f = (float)F.S;
+    F.part_len_f = (float)F.part_len;
+    F.part_len2_f = (float)F.part_len2;
+    F.inv_S_f = 1.0f / F.S_f;
+    F.inv_part_len_f = 1.0f / F.part_len_f;
+    F.inv_part_len2_f = 1.0f / F.part_len2_f;
     F.inv_S = inv_up(F.S);
     F.inv_W = inv_up(F.W);
     F.chunk_cap = fd->chunk_cap ? fd->chunk_cap : (tier == rtk::TIER_MESH ? RT_QUEUE_CHUNK_MESH : RT_QUEUE_CHUNK);
@@ -3333,7 +3357,8 @@ static hipError_t launch_reduce(const rtk_frame_desc* fd, const rtk::Frame& F, d
     const uint32_t npix = fd->W * fd->rows;
     const uint32_t reduce_waves = (npix + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
     hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((reduce_waves + 3) / 4), dim3(256), 0, stream, partial, npix, fd->S,
-                       F.parts, F.whole_items / fd->S, fd->pixel_sample_scale, out, srgb, toon);
+                       F.parts, F.whole_items / fd->S, F.parts2, F.fine_item0 / fd->S, fd->pixel_sample_scale, out,
+                       srgb, toon);
     return hipGetLastError();
 }
 
@@ -3459,6 +3484,34 @@ extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t p
     const uint64_t by_queue = (0xFFF00000ull - 1 - whole) / extra_row;
     if (t > by_queue) t = by_queue;
     return (uint32_t)t;
+}
+
+extern "C" void rtk_tail_split(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint32_t parts2,
+                               uint64_t budget_bytes, uint32_t permille, uint32_t fine_permille, uint32_t* tail,
+                               uint32_t* fine) {
+    *tail = *fine = 0;
+    if (parts <= 1 || W == 0 || S == 0) return;
+    const uint64_t whole = (uint64_t)W * H * S;
+    if (whole >= 0xFFF00000ull) return;
+    uint64_t room = 0xFFF00000ull - 1 - whole;  // queue entries beyond one per stratum row
+    uint64_t f = 0;
+    if (parts2 > parts) {
+        f = ((uint64_t)H * fine_permille + 999) / 1000;
+        if (f > H) f = H;
+        const uint64_t extra_f = (uint64_t)W * S * (parts2 - 1);
+        f = std::min<uint64_t>(f, (budget_bytes / 2) / (extra_f * 3 * sizeof(double)));
+        f = std::min<uint64_t>(f, (room / 2) / extra_f);
+        budget_bytes -= f * extra_f * 3 * sizeof(double);
+        room -= f * extra_f;
+    }
+    uint64_t tp = ((uint64_t)H * permille + 999) / 1000;  // the whole tail, fine rows included
+    if (tp > H) tp = H;
+    tp = tp > f ? tp - f : 0;  // its rows in `parts`
+    const uint64_t extra_row = (uint64_t)W * S * (parts - 1);
+    tp = std::min<uint64_t>(tp, budget_bytes / (extra_row * 3 * sizeof(double)));
+    tp = std::min<uint64_t>(tp, room / extra_row);
+    *fine = (uint32_t)f;
+    *tail = (uint32_t)(f + tp);
 }
 
 extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row_offset, uint32_t row_stride,

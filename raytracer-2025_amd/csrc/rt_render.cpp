@@ -138,7 +138,7 @@ struct DeviceWorld {
     // the last render on this slot
     bool ran = false;  // the path kernel ran (ev_start / ev_stop are valid)
     uint64_t samples = 0;
-    uint32_t W = 0, rows = 0, S = 0, parts = 1, whole_rows = 0;
+    uint32_t W = 0, rows = 0, S = 0, parts = 1, whole_rows = 0, parts2 = 1, fine_row = 0;
     hipStream_t last_stream = nullptr;
 };
 
@@ -636,11 +636,23 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     uint64_t budget = (uint64_t)env_u32("RT_PART_BUDGET_MB", 4096) << 20;
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) == hipSuccess && mem_total) budget = std::min<uint64_t>(budget, mem_total / 64);
-    f.parts = rtk_row_parts(f.S, env_u32("RT_PART_SAMPLES", 4));
-    const uint32_t tail = rtk_tail_rows(f.W, H, f.S, f.parts, budget, env_u32("RT_TAIL_PERMILLE", 500));
+    // The tail's last RT_FINE_PERMILLE / 1000 image rows (3 %) go out in
+    // parts of about RT_FINE_SAMPLES (1) samples: what is in flight when the
+    // queue runs dry is then one sample a lane, not a 4-sample part
+    // (DESIGN.md §4 "Fine rows").  The mesh tier's tail parts are 2 samples:
+    // its samples are long (dependent global loads per walk step), C4's 1/8
+    // shard 25.5 -> 24.5 ms and frame -1 %; C2 keeps 4 (its shard +2 % at 2).
+    f.parts = rtk_row_parts(f.S, env_u32("RT_PART_SAMPLES", d->tier == rtk::TIER_MESH ? 2 : 4));
+    f.parts2 = rtk_row_parts(f.S, env_u32("RT_FINE_SAMPLES", 1));
+    uint32_t tail = 0, fine = 0;
+    rtk_tail_split(f.W, H, f.S, f.parts, f.parts2, budget, env_u32("RT_TAIL_PERMILLE", 500),
+                   env_u32("RT_FINE_PERMILLE", 30), &tail, &fine);
     if (tail == 0) f.parts = 1;
-    // the shard's rows above the tail: image rows row_offset + r * row_stride < H - tail
+    if (fine == 0) f.parts2 = f.parts;
+    // the shard's rows above the tail (image rows row_offset + r * row_stride
+    // < H - tail), and above the fine rows
     f.whole_rows = rtk_shard_whole_rows(H, tail, f.row_offset, f.row_stride, f.rows);
+    f.fine_row = rtk_shard_whole_rows(H, fine, f.row_offset, f.row_stride, f.rows);
     // guided chunks of at least 64 entries, one per lane of the wave (DESIGN §4
     // "Tail rows": C2 -0.4 % frame, -2.3 % worst 1/8 shard; C3 -0.3 %; C4 +-0)
     f.chunk_min = env_u32("RT_CHUNK_MIN", 64);
@@ -648,14 +660,16 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     f.guide = env_u32("RT_CHUNK_GUIDE", 0);
     f.chunk_min_whole = env_u32("RT_CHUNK_MIN_WHOLE", 0);
     auto part_sums = [&f]() {
-        return ((size_t)f.W * f.whole_rows * f.S + (size_t)f.W * (f.rows - f.whole_rows) * f.S * f.parts) * 3 *
-               sizeof(double);
+        const size_t fr = std::max(f.fine_row, f.whole_rows);
+        return ((size_t)f.W * f.whole_rows * f.S + (size_t)f.W * (fr - f.whole_rows) * f.S * f.parts +
+                (size_t)f.W * (f.rows - fr) * f.S * f.parts2) *
+               3 * sizeof(double);
     };
     rc = grow((void**)&d->partial, d->partial_bytes, part_sums(), "hipMalloc partial sums");
     if (rc != RT_OK && f.parts > 1) {
         (void)hipGetLastError();
-        f.parts = 1;
-        f.whole_rows = f.rows;
+        f.parts = f.parts2 = 1;
+        f.whole_rows = f.fine_row = f.rows;
         rc = grow((void**)&d->partial, d->partial_bytes, part_sums(), "hipMalloc partial sums (whole rows)");
     }
     if (rc != RT_OK) return fail(rc);
@@ -720,6 +734,8 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     d->S = f.S;
     d->parts = f.parts;
     d->whole_rows = f.parts > 1 ? f.whole_rows : f.rows;
+    d->parts2 = f.parts > 1 ? f.parts2 : 1u;
+    d->fine_row = f.parts > 1 ? std::max(f.fine_row, d->whole_rows) : f.rows;
     d->last_stream = p.stream;
 }
 
@@ -1081,10 +1097,13 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
     hipError_t e = hipStreamSynchronize(d->last_stream);
     if (e != hipSuccess) return hip_fail(e, "render (stream synchronize)");
     // device slots in queue order (rtk::Frame): one per stratum row of the
-    // whole rows, `parts` per stratum row of the tail rows; a tail row's sum =
-    // its part sums added in part order, as rt_reduce_kernel adds them
+    // whole rows, `parts` per stratum row of the tail rows, `parts2` per
+    // stratum row of the fine rows; a tail row's sum = its part sums added in
+    // part order, as rt_reduce_kernel adds them
     const uint64_t npix = (uint64_t)d->W * d->rows, whole_px = (uint64_t)d->W * d->whole_rows;
-    const uint64_t slots = whole_px * d->S + (npix - whole_px) * d->S * d->parts;
+    const uint64_t fine_px = (uint64_t)d->W * d->fine_row;
+    const uint64_t fine_first = whole_px * d->S + (fine_px - whole_px) * d->S * d->parts;
+    const uint64_t slots = fine_first + (npix - fine_px) * d->S * d->parts2;
     std::vector<double> buf;
     try {
         buf.resize(slots * 3);
@@ -1094,9 +1113,11 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {
     if (n && (e = hipMemcpy(buf.data(), d->partial, buf.size() * sizeof(double), hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "hipMemcpy partials");
     for (uint64_t pix = 0; pix < npix; ++pix) {
-        const bool whole = pix < whole_px;
-        const uint32_t np = whole ? 1u : d->parts;
-        const double* px = buf.data() + (whole ? pix * d->S : whole_px * d->S + (pix - whole_px) * d->S * np) * 3;
+        const bool whole = pix < whole_px, fine = pix >= fine_px;
+        const uint32_t np = whole ? 1u : (fine ? d->parts2 : d->parts);
+        const double* px = buf.data() + (whole ? pix * d->S
+                                         : fine ? fine_first + (pix - fine_px) * d->S * np
+                                                : whole_px * d->S + (pix - whole_px) * d->S * np) * 3;
         for (uint32_t si = 0; si < d->S; ++si)
             for (int c = 0; c < 3; ++c) {
                 const double* src = px + (uint64_t)si * np * 3 + c;

@@ -99,3 +99,40 @@ def test_shard_tails_are_each_shards_last_rows(lib, H, tail):
             assert all(y < H - tail for y in img[:w]) and all(y >= H - tail for y in img[w:])
             total += w
         assert total == H - tail
+
+
+def _split(lib, W, H, S, parts, parts2, budget, permille, fine_permille):
+    f = lib.rtk_tail_split
+    f.restype = None
+    f.argtypes = [ctypes.c_uint32] * 5 + [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    t, fi = ctypes.c_uint32(), ctypes.c_uint32()
+    f(W, H, S, parts, parts2, budget, permille, fine_permille, ctypes.byref(t), ctypes.byref(fi))
+    return t.value, fi.value
+
+
+@pytest.mark.parametrize("W,H,S", [(1920, 1080, 22), (800, 800, 32), (1920, 1080, 16), (3840, 2160, 64),
+                                   (16, 9, 4), (1920, 1080, 100)])
+@pytest.mark.parametrize("budget", [GiB // 4, 4 * GiB, 1 << 62])
+def test_fine_rows_are_the_last_rows_of_the_tail(lib, W, H, S, budget):
+    """rtk_tail_split: the fine rows (parts of ~1 sample) are the frame's last
+    rows, inside the tail (fine <= tail <= H), about the asked shares, their
+    extra part sums within half the budget and the whole split's within the
+    budget and the 2^32 queue; with no finer parts asked it is rtk_tail_rows."""
+    p, p2 = lib.rtk_row_parts(S, 4), lib.rtk_row_parts(S, 1)
+    t, fi = _split(lib, W, H, S, p, p2, budget, 500, 30)
+    assert fi <= t <= H
+    assert fi <= -(-H * 30 // 1000)
+    if p2 > p:
+        assert fi * W * S * (p2 - 1) * 24 <= budget // 2
+    extra = fi * W * S * (p2 - 1) + (t - fi) * W * S * (p - 1)
+    assert extra * 24 <= budget
+    assert W * H * S + extra < 0xFFF00000
+    if budget == 1 << 62 and p > 1 and W * H * S * p2 < 0xFFF00000 // 2:
+        assert fi == -(-H * 30 // 1000) and t == max(fi, -(-H * 500 // 1000))
+    # no finer parts: the old tail, no fine rows
+    t0, f0 = _split(lib, W, H, S, p, p, budget, 500, 30)
+    assert f0 == 0 and t0 == lib.rtk_tail_rows(W, H, S, p, budget, 500)
+    # C4 (1920 x 1080 at 16^2, 4 GiB): 33 fine rows of 16 one-sample parts
+    if (W, H, S, budget) == (1920, 1080, 16, 4 * GiB):
+        assert (t, fi) == (540, 33)
