@@ -51,6 +51,8 @@ namespace rtk {
 struct Diag {
 #ifdef RT_DIAG
     unsigned long long cyc_refill = 0, cyc_trace = 0, cyc_shade = 0, cyc_media = 0;
+    // basic / mesh tiers' unified loop: the parts of cyc_refill after the walk
+    unsigned long long cyc_miss = 0, cyc_queue = 0, cyc_draws = 0;
     unsigned long long wave_trace_iters = 0, lane_trace_iters = 0, node_visits = 0, sphere_tests = 0, main_iters = 0;
     unsigned long long load_cyc = 0, loads = 0;  // -DRT_DIAG_LOADLAT: node-load latency (first active lane)
     unsigned long long pops = 0, pop_reads = 0;  // basic tier: pops and the stack entries they read
@@ -2419,7 +2421,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 finish_sample();
                 cam = true;
             }
+            RT_DIAG_ONLY(const unsigned long long t_m = __builtin_amdgcn_s_memtime(); dg.cyc_miss += t_m - t_b1;)
             if (!refill()) break;
+            RT_DIAG_ONLY(const unsigned long long t_q = __builtin_amdgcn_s_memtime(); dg.cyc_queue += t_q - t_m;)
             if (carry) continue;
             // the iteration's draws: a hit's (vertex, slots 0 and 1) or a new
             // sample's camera draws (vertex 0: theta and r of the defocus disk
@@ -2428,7 +2432,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             Draws Dr;
             rng.pair(cam ? 0u : vertex, (cam && F.defocus) ? 1u : 0u, Dr.xi0, Dr.xi1);
             k_sincos(2.0 * PI * Dr.xi0, &Dr.sn, &Dr.cs);
-            RT_DIAG_ONLY(const unsigned long long t_d = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_d - t_b1;)
+            RT_DIAG_ONLY(const unsigned long long t_d = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_d - t_b1;
+                         dg.cyc_draws += t_d - t_q;)
             if (!cam) {
                 // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
                 rng.begin(vertex);
@@ -2706,6 +2711,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         atomicAdd(&g_diag[2], dg.cyc_shade);
         atomicAdd(&g_diag[4], dg.main_iters);
         atomicAdd(&g_diag[13], dg.cyc_media);
+        atomicAdd(&g_diag[21], dg.cyc_miss);
+        atomicAdd(&g_diag[22], dg.cyc_queue);
+        atomicAdd(&g_diag[23], dg.cyc_draws);
     }
     atomicAdd(&g_diag[3], dg.wave_trace_iters);  // counted by the first active lane of each wave iteration
     atomicAdd(&g_diag[5], dg.lane_trace_iters);

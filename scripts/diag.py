@@ -67,6 +67,11 @@ out = {
     "uniform_node_step_share": c[18] / c[16] if c[16] else None,
     "lanes_on_first_record": c[20] / c[19] if c[19] else None,
     "active_lanes_per_step": c[19] / c[16] if c[16] else None,
+    # basic / mesh tiers' unified loop: shares of all wave cycles after the
+    # walk -- a miss's sky and the sample's end, the queue refill, the
+    # iteration's Philox block and sincos (the rest of refill+camera: the
+    # walk set-up and the camera rays)
+    "after_walk_share": {"miss+finish": c[21] / tot, "queue_refill": c[22] / tot, "draws": c[23] / tot},
     "raw": c[:24],
 }
 print(json.dumps(out, indent=1))
