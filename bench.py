@@ -124,7 +124,12 @@ def _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads):
     t0 = time.perf_counter()
     api.check(api.render_f64(scene.s, world.h, -1 if lights is None else lights.h, ctypes.byref(c), ctypes.byref(opts),
                              None, None, ctypes.byref(st), None))
-    return st.samples, time.perf_counter() - t0
+    dt = time.perf_counter() - t0
+    # a progress line per CPU run (each well under the GPU box's 3-minute
+    # silence limit; C5's baseline is several of them)
+    print(f"bench.py: cpu baseline run: {threads} threads, every {row_stride}th row, {dt:.1f} s",
+          file=sys.stderr, flush=True)
+    return st.samples, dt
 
 
 def physical_cores():
