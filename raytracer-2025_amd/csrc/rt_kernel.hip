@@ -77,6 +77,29 @@ __device__ unsigned long long g_diag[RT_DIAG_N];
 // lane's last refill, s_memtime ticks from start to end} (scripts/lane_trace.py)
 constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 10;
 __device__ unsigned long long g_lane_trace[RT_TRACE_LANES * RT_TRACE_W];
+// ... and the rays begun per 0.25 ms of the launch (each wave's own clock
+// from its start; one atomic per wave and bucket): the launch's throughput
+// over time -- its ramp, steady state and drain
+constexpr uint32_t RT_HIST_N = 1024, RT_HIST_TICKS = 25000;  // s_memrealtime: 100 MHz
+__device__ unsigned long long g_ray_hist[RT_HIST_N];
+struct RayHist {
+    unsigned long long t0;
+    uint32_t bucket = 0, count = 0;
+    // beg: the lanes of the wave beginning a ray now (wave-uniform)
+    __device__ __forceinline__ void add(unsigned long long beg) {
+        const uint32_t b = min((uint32_t)((__builtin_amdgcn_s_memrealtime() - t0) / RT_HIST_TICKS), RT_HIST_N - 1);
+        if (b != bucket) {
+            flush();
+            bucket = b;
+        }
+        count += (uint32_t)__popcll(beg);
+    }
+    __device__ __forceinline__ void flush() {
+        if (count && __lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1))
+            atomicAdd(&g_ray_hist[bucket], (unsigned long long)count);
+        count = 0;
+    }
+};
 #endif
 
 struct Ray {
@@ -2273,6 +2296,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long trace_c0 = __builtin_amdgcn_s_memtime();
     uint32_t trace_items = 0, trace_q = 0, trace_rays = 0, trace_steps = 0, trace_steps_q = 0;
+    RayHist hist;
+    hist.t0 = __builtin_amdgcn_readfirstlane(trace_t0);
     unsigned long long trace_tq = trace_t0;
 #endif
     // ---- refill: the lanes that need a queue entry take one (false: the
@@ -2369,6 +2394,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC : RT_SHADE_BATCH_MESH;
         for (;;) {
             RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
+#ifdef RT_WAVE_TRACE
+            hist.add(__ballot(!no_path && !walking));
+#endif
             if (!no_path) {
                 if (!walking) {
                     rng.begin(vertex);
@@ -2582,6 +2610,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         // lanes have finished (or none walks any more); those are shaded and get
         // their next ray while the unfinished walks carry over to the next round,
         // so short walks do not idle behind the longest one of the wave.
+#ifdef RT_WAVE_TRACE
+        hist.add(__ballot(!walking));
+#endif
         if (!walking) {
             rng.begin(vertex);
             ++n_rays;
@@ -2733,6 +2764,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     atomicAdd(&g_diag[20], dg.u_same);
 #endif
 #ifdef RT_WAVE_TRACE
+    hist.flush();
     if (trace_lane < RT_TRACE_LANES) {
         unsigned long long* t = g_lane_trace + (uint64_t)trace_lane * RT_TRACE_W;
         t[0] = trace_t0;
@@ -3118,6 +3150,13 @@ extern "C" int rt_lane_trace(unsigned long long* out, uint64_t n_lanes) {
     if (n_lanes > rtk::RT_TRACE_LANES) n_lanes = rtk::RT_TRACE_LANES;
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_lane_trace),
                                     n_lanes * rtk::RT_TRACE_W * sizeof(unsigned long long));
+}
+// the rays-begun histogram (RT_HIST_N buckets of 0.25 ms); out == NULL: zero it
+extern "C" int rt_ray_hist(unsigned long long* out, uint64_t n) {
+    static const unsigned long long zero[rtk::RT_HIST_N] = {};
+    if (!out) return (int)hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_ray_hist), zero, sizeof zero);
+    if (n > rtk::RT_HIST_N) n = rtk::RT_HIST_N;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_ray_hist), n * sizeof(unsigned long long));
 }
 #endif
 #if defined(RT_CHECK)

@@ -29,6 +29,7 @@ def main():
     torch.cuda.init()
     lib = ctypes.CDLL(os.path.join(ROOT, "raytracer-2025_amd", os.environ.get("TRACE_LIB", "librt_mi355x_trace.so")))
     lib.rt_lane_trace.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint64]
+    lib.rt_ray_hist.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_uint64]
     api = capi.Api(lib, "rt_")
     s = rt.Scene(api)
     world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
@@ -38,8 +39,11 @@ def main():
     for stride in strides:
         ctypes.memset(buf, 0, ctypes.sizeof(buf))
         torch.cuda.synchronize()
+        assert lib.rt_ray_hist(None, 0) == 0
         _, _, st = cam.render(world, lights, seed=1, row_stride=stride, want_srgb=False)
         assert lib.rt_lane_trace(buf, n) == 0
+        hist = (ctypes.c_ulonglong * 1024)()
+        assert lib.rt_ray_hist(hist, 1024) == 0
         a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
         a = a[a[:, 1] > 0]
         t0, t1 = a[:, 0].min(), a[:, 1].max()
@@ -59,6 +63,15 @@ def main():
             "rays_per_lane": {"min": int(a[:, 3].min()), "mean": round(float(a[:, 3].mean()), 1),
                               "max": int(a[:, 3].max())},
         }
+        # rays begun per 0.25 ms of the launch, as a fraction of the launch's
+        # median rate: the ramp (first ms), steady state and drain
+        h = np.frombuffer(hist, dtype=np.uint64).astype(np.float64)
+        nb = int(np.nonzero(h)[0].max()) + 1 if h.any() else 0
+        med = float(np.median(h[:nb])) if nb else 1.0
+        rec["rays_per_quarter_ms_vs_median"] = {"first_8": [round(x / med, 3) for x in h[:8]],
+                                                "last_8": [round(x / med, 3) for x in h[max(0, nb - 8):nb]],
+                                                "buckets": nb, "median_rays": med,
+                                                "lost_vs_median_ms": round(float(np.sum(np.maximum(0.0, med - h[:nb]))) / med * 0.25, 3)}
         # the last lanes to finish: when they took their last queue entry, which
         # one (pixel row of the shard, stratum row / part), rays since then
         S = cam.sqrt_spp
