@@ -2297,7 +2297,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     const unsigned long long trace_c0 = __builtin_amdgcn_s_memtime();
     uint32_t trace_items = 0, trace_q = 0, trace_rays = 0, trace_steps = 0, trace_steps_q = 0;
     RayHist hist;
-    hist.t0 = __builtin_amdgcn_readfirstlane(trace_t0);
+    hist.t0 = trace_t0;  // (an s_memrealtime: one value per wave)
     unsigned long long trace_tq = trace_t0;
 #endif
     // ---- refill: the lanes that need a queue entry take one (false: the

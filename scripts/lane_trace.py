@@ -67,10 +67,12 @@ def main():
         # median rate: the ramp (first ms), steady state and drain
         h = np.frombuffer(hist, dtype=np.uint64).astype(np.float64)
         nb = int(np.nonzero(h)[0].max()) + 1 if h.any() else 0
-        med = float(np.median(h[:nb])) if nb else 1.0
+        med = float(np.median(h[:nb][h[:nb] > 0])) if nb else 0.0
+        med = med if med > 0 else 1.0
         rec["rays_per_quarter_ms_vs_median"] = {"first_8": [round(x / med, 3) for x in h[:8]],
                                                 "last_8": [round(x / med, 3) for x in h[max(0, nb - 8):nb]],
-                                                "buckets": nb, "median_rays": med,
+                                                "buckets": nb, "nonzero": int(np.count_nonzero(h)),
+                                                "rays": float(h.sum()), "median_rays": med,
                                                 "lost_vs_median_ms": round(float(np.sum(np.maximum(0.0, med - h[:nb]))) / med * 0.25, 3)}
         # the last lanes to finish: when they took their last queue entry, which
         # one (pixel row of the shard, stratum row / part), rays since then
