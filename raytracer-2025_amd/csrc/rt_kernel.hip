@@ -3234,13 +3234,13 @@ __device__ __forceinline__ uint8_t srgb_u8(double x, int toon) {
 // runs of 24 B and its next loads the same lines (one lane per pixel read 64
 // lines per load, three times: 1.8 ms for C2's 3.8 GB against 0.8 at HBM rate).
 constexpr uint32_t REDUCE_PX_PER_WAVE = 21;
-__global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t npix, uint32_t S,
-                                                       uint32_t parts, uint32_t whole_px, uint32_t parts2,
+__global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict__ partial, uint32_t p_lo, uint32_t npix,
+                                                       uint32_t S, uint32_t parts, uint32_t whole_px, uint32_t parts2,
                                                        uint32_t fine_px, double scale, float* __restrict__ out,
                                                        uint8_t* __restrict__ srgb, int toon) {
     const uint32_t lane = threadIdx.x & 63u, wave = blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u;
     if (lane >= 3u * REDUCE_PX_PER_WAVE) return;
-    const uint32_t p = wave * REDUCE_PX_PER_WAVE + lane / 3u, c = lane % 3u;
+    const uint32_t p = p_lo + wave * REDUCE_PX_PER_WAVE + lane / 3u, c = lane % 3u;  // pixels [p_lo, npix)
     if (p >= npix) return;
     // pixels [0, whole_px): one sum per stratum row; [whole_px, fine_px):
     // `parts`; [fine_px, npix): `parts2` (the fine rows)
@@ -3261,6 +3261,63 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     const double v = acc * scale;
     out[(uint64_t)p * 3 + c] = (float)v;
     if (srgb) srgb[(uint64_t)p * 3 + c] = srgb_u8(v, toon);
+}
+
+// The same sums, staged through LDS (RT_REDUCE_LDS): one wave per group of
+// `pw` consecutive pixels of one region (whole rows: np = 1; tail rows: np =
+// parts; fine rows: np = parts2), whose part sums are contiguous in slot
+// order.  The wave copies the group's doubles into LDS with whole-line loads
+// (each lane 8 B, 64 lanes 512 B a step), adds each (pixel, s_i, channel)'s
+// parts in part order into the slot of part 0, then each (pixel, channel)'s
+// S row sums in s_i order -- rt_reduce_kernel's additions in its order, so
+// the same bits -- where that kernel's lanes read 21 pixels' 24-B runs per
+// load and re-read each line from the cache several times.
+constexpr uint32_t REDUCE_LDS_DOUBLES = 2048;  // 16 KiB per wave
+__global__ void __launch_bounds__(64) rt_reduce_lds_kernel(const double* __restrict__ partial, uint32_t p_begin,
+                                                          uint32_t p_end, uint64_t slot0, uint32_t S, uint32_t np,
+                                                          uint32_t pw, double scale, float* __restrict__ out,
+                                                          uint8_t* __restrict__ srgb, int toon) {
+    __shared__ double buf[REDUCE_LDS_DOUBLES];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t p0 = p_begin + blockIdx.x * pw;
+    if (p0 >= p_end) return;
+    const uint32_t n = min(pw, p_end - p0);
+    const uint32_t row = np * 3u;          // doubles per stratum row
+    const uint32_t per_px = S * row;       // doubles per pixel
+    const uint32_t total = n * per_px;     // <= REDUCE_LDS_DOUBLES (host)
+    const double* src = partial + (slot0 + (uint64_t)(p0 - p_begin) * S * np) * 3u;
+    // (8 loads in flight per lane before their LDS stores)
+    uint32_t i0 = lane;
+    for (; i0 + 7u * 64u < total; i0 += 8u * 64u) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[i0 + u * 64u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) buf[i0 + u * 64u] = v[u];
+    }
+    for (; i0 < total; i0 += 64u) buf[i0] = src[i0];
+    __syncthreads();
+    if (np > 1u) {
+        // (pixel, s_i, channel): its parts in order, into part 0's slot
+        for (uint32_t i = lane; i < n * S * 3u; i += 64u) {
+            const uint32_t c = i % 3u, ps = i / 3u;  // ps = pixel * S + s_i
+            double* r = buf + ps * row + c;
+            double rr = r[0];
+            for (uint32_t j = 1; j < np; ++j) rr += r[j * 3u];
+            r[0] = rr;
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = lane; i < n * 3u; i += 64u) {
+        const uint32_t c = i % 3u, px = i / 3u;
+        const double* r = buf + px * per_px + c;
+        double acc = 0.0;
+        for (uint32_t k = 0; k < S; ++k) acc += r[k * row];
+        const double v = acc * scale;
+        const uint64_t o = (uint64_t)(p0 + px) * 3u + c;
+        out[o] = (float)v;
+        if (srgb) srgb[o] = srgb_u8(v, toon);
+    }
 }
 
 // Math self-test (rt_math_selftest): the kernel's f64 functions (impl 0,
@@ -3409,11 +3466,42 @@ static void fill_kparams(rtk::KParams& K, const rtk::SceneView* view, const rtk_
     K.stack_ovf = (RT_GLOBAL uint2*)stack_ovf;
 }
 
+#ifndef RT_REDUCE_LDS
+#define RT_REDUCE_LDS 1
+#endif
 static hipError_t launch_reduce(const rtk_frame_desc* fd, const rtk::Frame& F, double* partial, float* out,
                                 uint8_t* srgb, int toon, hipStream_t stream) {
     const uint32_t npix = fd->W * fd->rows;
+    if (RT_REDUCE_LDS) {
+        // the three regions of the slot order (rtk::Frame): whole rows, tail
+        // parts, fine parts; a region whose pixel does not fit the wave's LDS
+        // (S x np x 24 B > 16 KiB, e.g. C5's 64 x 16 tail parts) takes the
+        // direct kernel for the whole frame
+        const uint32_t whole_px = F.whole_items / fd->S, fine_px = F.fine_item0 / fd->S;
+        const struct { uint32_t b, e, np; } reg[3] = {
+            {0u, whole_px, 1u}, {whole_px, fine_px, F.parts}, {fine_px, npix, F.parts2}};
+        uint64_t slot = 0;
+        for (const auto& r : reg) {
+            if (r.e > r.b) {
+                const uint64_t dpp = (uint64_t)fd->S * r.np * 3u;  // doubles per pixel
+                if (dpp <= rtk::REDUCE_LDS_DOUBLES) {
+                    const uint32_t pw = (uint32_t)std::min<uint64_t>(64u, rtk::REDUCE_LDS_DOUBLES / dpp);
+                    const uint32_t groups = (r.e - r.b + pw - 1u) / pw;
+                    hipLaunchKernelGGL(rtk::rt_reduce_lds_kernel, dim3(groups), dim3(64), 0, stream, partial, r.b,
+                                       r.e, slot, fd->S, r.np, pw, fd->pixel_sample_scale, out, srgb, toon);
+                } else {
+                    const uint32_t waves = (r.e - r.b + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
+                    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, partial,
+                                       r.b, r.e, fd->S, F.parts, whole_px, F.parts2, fine_px,
+                                       fd->pixel_sample_scale, out, srgb, toon);
+                }
+            }
+            slot += (uint64_t)(r.e - r.b) * fd->S * r.np;
+        }
+        return hipGetLastError();
+    }
     const uint32_t reduce_waves = (npix + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
-    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((reduce_waves + 3) / 4), dim3(256), 0, stream, partial, npix, fd->S,
+    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((reduce_waves + 3) / 4), dim3(256), 0, stream, partial, 0u, npix, fd->S,
                        F.parts, F.whole_items / fd->S, F.parts2, F.fine_item0 / fd->S, fd->pixel_sample_scale, out,
                        srgb, toon);
     return hipGetLastError();
