@@ -75,7 +75,7 @@ __device__ unsigned long long g_diag[RT_DIAG_N];
 // trace build: per lane of the grid, {start, end (s_memrealtime, 100 MHz),
 // queue entries taken, rays traced, time / queue entry / rays so far at the
 // lane's last refill, s_memtime ticks from start to end} (scripts/lane_trace.py)
-constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 10;
+constexpr uint32_t RT_TRACE_LANES = 1u << 19, RT_TRACE_W = 12;
 __device__ unsigned long long g_lane_trace[RT_TRACE_LANES * RT_TRACE_W];
 // ... and the rays begun per 0.25 ms of the launch (each wave's own clock
 // from its start; one atomic per wave and bucket): the launch's throughput
@@ -2306,6 +2306,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
     const unsigned long long trace_c0 = __builtin_amdgcn_s_memtime();
     uint32_t trace_items = 0, trace_q = 0, trace_rays = 0, trace_steps = 0, trace_steps_q = 0;
+    // the wave's queue atomics: count and the ticks from issue to return
+    // (wave-uniform; every lane holds the wave's value)
+    unsigned long long trace_atomic_ticks = 0, trace_atomic_first = 0;
+    uint32_t trace_atomics = 0;
     RayHist hist;
     hist.t0 = trace_t0;  // (an s_memrealtime: one value per wave)
     unsigned long long trace_tq = trace_t0;
@@ -2340,8 +2344,18 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if (avail < n) {
                 if (!dry) {
                     const uint32_t leader = __ffsll((long long)mask) - 1;
+#ifdef RT_WAVE_TRACE
+                    const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
+#endif
                     if (need && rank == 0) fresh = atomicAdd(queue, chunk);
                     fresh = __builtin_amdgcn_readlane(fresh, leader) + F.static_entries;
+#ifdef RT_WAVE_TRACE
+                    {
+                        const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
+                        trace_atomic_ticks += tb - ta;
+                        if (trace_atomics++ == 0) trace_atomic_first = tb - trace_t0;
+                    }
+#endif
                     dry = fresh + chunk >= F.queue_total;
                 } else {
                     fresh = F.queue_total;  // past the end: the needy lanes leave
@@ -2544,8 +2558,18 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if (avail < n) {
                 if (!dry) {
                     const uint32_t leader = __ffsll((long long)mask) - 1;
+#ifdef RT_WAVE_TRACE
+                    const unsigned long long ta = __builtin_amdgcn_s_memrealtime();
+#endif
                     if (need && rank == 0) fresh = atomicAdd(queue, chunk);
                     fresh = __builtin_amdgcn_readlane(fresh, leader) + F.static_entries;
+#ifdef RT_WAVE_TRACE
+                    {
+                        const unsigned long long tb = __builtin_amdgcn_s_memrealtime();
+                        trace_atomic_ticks += tb - ta;
+                        if (trace_atomics++ == 0) trace_atomic_first = tb - trace_t0;
+                    }
+#endif
                     dry = fresh + chunk >= F.queue_total;
                 } else {
                     fresh = F.queue_total;  // past the end: the needy lanes leave
@@ -2787,6 +2811,8 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         t[7] = __builtin_amdgcn_s_memtime() - trace_c0;  // shader clocks over the lane's life
         t[8] = trace_steps;  // walk steps (wave iterations the lane walked in)
         t[9] = trace_steps_q;  // ... at its last refill
+        t[10] = trace_atomic_ticks | ((unsigned long long)trace_atomics << 40);  // wave's atomic wait, count
+        t[11] = trace_atomic_first;  // when the wave's first atomic returned (ticks after its start)
     }
 #endif
     // one atomic per wave, not per lane: 262 144 adds to one address at the

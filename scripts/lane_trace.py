@@ -35,7 +35,7 @@ def main():
     world, lights, cam, desc = bench.build_workload(scenes, s, wl, bench.WORKLOADS[wl][0], spp)
     cam.render(world, lights, seed=1, want_srgb=False)
     n = 1 << 19
-    buf = (ctypes.c_ulonglong * (n * 10))()
+    buf = (ctypes.c_ulonglong * (n * 12))()
     for stride in strides:
         ctypes.memset(buf, 0, ctypes.sizeof(buf))
         torch.cuda.synchronize()
@@ -44,7 +44,7 @@ def main():
         assert lib.rt_lane_trace(buf, n) == 0
         hist = (ctypes.c_ulonglong * 1024)()
         assert lib.rt_ray_hist(hist, 1024) == 0
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 10).astype(np.int64)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 12).astype(np.int64)
         a = a[a[:, 1] > 0]
         t0, t1 = a[:, 0].min(), a[:, 1].max()
         span = (t1 - t0) / 100.0  # 100 MHz -> us
@@ -63,6 +63,19 @@ def main():
             "rays_per_lane": {"min": int(a[:, 3].min()), "mean": round(float(a[:, 3].mean()), 1),
                               "max": int(a[:, 3].max())},
         }
+        # the waves' queue atomics: per wave (lane 0 of each wave), the wait
+        # from issue to return summed over the launch, the count, and when
+        # the first one returned
+        w0 = a[::64]
+        wait_ms = (w0[:, 10] & ((1 << 40) - 1)) / 1e5
+        cnt = w0[:, 10] >> 40
+        first = w0[:, 11] / 1e5
+        rec["queue_atomics_per_wave"] = {
+            "count_mean": round(float(cnt.mean()), 2), "count_max": int(cnt.max()),
+            "wait_ms_mean": round(float(wait_ms.mean()), 4), "wait_ms_max": round(float(wait_ms.max()), 4),
+            "wait_share_of_span": round(float(wait_ms.mean()) / (span / 1e3), 4),
+            "first_return_ms_pct": {p: round(float(np.percentile(first[cnt > 0], p)), 3) for p in (1, 50, 99, 100)}
+            if (cnt > 0).any() else None}
         # rays begun per 0.25 ms of the launch, as a fraction of the launch's
         # median rate: the ramp (first ms), steady state and drain
         h = np.frombuffer(hist, dtype=np.uint64).astype(np.float64)
