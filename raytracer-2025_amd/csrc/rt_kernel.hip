@@ -2710,7 +2710,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         }
         RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
         if constexpr (BATCH < 64 && tier_full(TIER)) {
+            RT_DIAG_ONLY(const unsigned long long t_mb = __builtin_amdgcn_s_memtime();)
             if (!walking) media_phase<TIER>(S, ray, T, stk, rng, med);
+            RT_DIAG_ONLY(dg.cyc_media += __builtin_amdgcn_s_memtime() - t_mb;)
         }
         if (BATCH < 64 && walking) {
             if constexpr (PARK) trace_park(T, pk);

@@ -49,7 +49,7 @@ out = {
     "samples": st.samples,
     "rays": st.rays,
     "cycle_share": {"refill+camera": c[0] / tot, "trace": c[1] / tot, "shade": c[2] / tot,
-                    "of which media_phase (full tiers, whole-wave shading)": c[13] / tot},
+                    "of which media_phase (full tiers)": c[13] / tot},
     "trace_lane_efficiency": c[5] / (64.0 * c[3]) if c[3] else None,
     "trace_iters_per_ray": c[5] / c[8],
     "wave_trace_iters_per_wave_bounce": c[3] / max(1, c[4]),
