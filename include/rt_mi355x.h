@@ -259,7 +259,8 @@ int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values);
 /* Test hook (parity tooling, not part of the reference surface): n calls of
  * one f64 function on the current gfx950 device, from host arrays a (and b)
  * into out.  fn: 0 sin, 1 cos, 2 sincos's sin, 3 sincos's cos, 4 log (ln),
- * 5 acos, 6 atan2(a, b), 7 sqrt.  impl 0: the functions the render kernel
+ * 5 acos, 6 atan2(a, b), 7 sqrt, 8 / 9 sin / cos of 2 pi a (a a unit draw,
+ * the path's sincos_2pi).  impl 0: the functions the render kernel
  * calls (rt_crmath.h: correctly rounded, in place of Rust's f64::sin / cos /
  * ln / acos / atan2 = glibc's); impl 1: ROCm's device libm (ocml).  Blocking. */
 int32_t rt_math_selftest(int32_t fn, int32_t impl, const double* a, const double* b, double* out, uint64_t n);

@@ -17,7 +17,8 @@
 //   sin / cos: x = k pi/128 + r, |r| <= pi/256 (Cody-Waite with a 26-bit first
 //     constant below 2^20, Payne-Hanek with the 128/pi bits above), then
 //     sin x = S cos r + C sin r with S, C = sin / cos(k pi/128) from a
-//     256-record table (8 KiB, L1-resident).
+//     256-record table (8 KiB, L1-resident); sincos_2pi(xi) for the path's
+//     x = 2 pi xi in [0, 2pi] with 44-bit constants and no range branches.
 //   log: x = 2^e z, r = z c - 1 exact as a double-double (|r| < 2^-7), then
 //     log x = e ln2 - log c + log1p(r); c = 1 around 1, so log x near 1 is
 //     log1p(r) without cancellation.
@@ -297,10 +298,9 @@ struct ScR {
     double rh, rl, hq, cmr, t;
     int k;
 };
-RTCR_FN bool sc_prep(double x, ScR& p) {
+// the polynomial pieces from p.rh, p.rl
+RTCR_FN void sc_poly(ScR& p) {
     RTCR_NOCONTRACT
-    if (!(abs_(x) <= 0x1p20) || abs_(x) < 0x1p-500) return false;
-    reduce_fast(x, p.rh, p.rl, p.k);
     const double rh = p.rh;
     const double q2 = rh * rh;
     const double eq = fma_(2.0 * rh, p.rl, fma_(rh, rh, -q2));  // r^2 = q2 + eq
@@ -308,6 +308,11 @@ RTCR_FN bool sc_prep(double x, ScR& p) {
     p.t = rh * ps;  // sin r - r
     p.hq = -0.5 * q2;
     p.cmr = fma_(q2 * q2, RTCR_C4_H + q2 * (RTCR_C6_H + q2 * RTCR_C8_H), -0.5 * eq);  // cos r - 1 - hq
+}
+RTCR_FN bool sc_prep(double x, ScR& p) {
+    if (!(abs_(x) <= 0x1p20) || abs_(x) < 0x1p-500) return false;
+    reduce_fast(x, p.rh, p.rl, p.k);
+    sc_poly(p);
     return true;
 }
 
@@ -348,6 +353,47 @@ RTCR_FN void sincos(double x, double* s, double* c) {
             *c = yc;
             return;
         }
+    }
+    sincos_slow(x, s, c);
+}
+
+// sin and cos of x = 2pi xi for 0 <= xi <= 1 (a unit draw: every sincos of
+// the path, vec3.rs:63-69 / 313-343, pdf.rs, camera.rs:263-266) -- the same
+// correctly rounded doubles as sincos(2.0 * PI * xi), with the argument's range
+// known: no range branches, and a reduction whose constants have 44 bits, so
+// that k C1 and k C2 are exact for k <= 256 (rt_crmath_tables.h): x - k C1
+// exact (Sterbenz, or one binade for k = 1), x - k C1 - k C2 as an exact two-sum,
+// lo = RN(s.l - k C3) (|error| < 2^-112), then a fast two-sum -- valid because
+// every double x lies >= 9.7e-21 from the k pi/128 it reduces to, far above
+// |lo| (scripts/gen_crmath_tables.py checks it).  x = 0 fails the rounding test
+// (err > 0) and takes the slow path, which returns sin 0 = 0, cos 0 = 1.
+RTCR_FN void reduce_2pi(double x, double& rh, double& rl, int& k) {
+    RTCR_NOCONTRACT
+    const double kd = __builtin_rint(x * RTCR_INV_PIO128);
+    const double y1 = fma_(-kd, RTCR_PIO128S_1, x);
+    const double p2 = kd * RTCR_PIO128S_2;
+    const DD s = two_sum(y1, -p2);
+    const double lo = fma_(-kd, RTCR_PIO128S_3, s.l);
+    const DD r = fast_two_sum(s.h, lo);
+    rh = r.h;
+    rl = r.l;
+    k = (int)kd;
+}
+RTCR_FN void sincos_2pi(double xi, double* s, double* c) {
+    RTCR_NOCONTRACT
+    const double x = 2.0 * 0x1.921fb54442d18p+1 * xi;  // 2.0 * PI * xi, PI = RN(pi)
+    ScR p;
+    reduce_2pi(x, p.rh, p.rl, p.k);
+    sc_poly(p);
+    DD S, C;
+    sc_table(p.k, S, C);
+    double ys, yc;
+    const bool oks = sc_combine(S, C, p.rh, p.rl, p.hq, p.cmr, p.t, ys);
+    const bool okc = sc_combine(C, dd_neg(S), p.rh, p.rl, p.hq, p.cmr, p.t, yc);
+    if (oks && okc) {
+        *s = ys;
+        *c = yc;
+        return;
     }
     sincos_slow(x, s, c);
 }

@@ -1721,9 +1721,8 @@ __device__ __forceinline__ D3 light_random_one(const SceneView& S, uint32_t ref,
     const D3 nd = unit(direction, ok1);
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
     const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
-    const double phi = 2.0 * PI * r1;
     double sphi, cphi;
-    k_sincos(phi, &sphi, &cphi);
+    k_sincos_2pi(r1, &sphi, &cphi);  // phi = 2.0 * PI * r1
     const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
     const D3 wv = onb_world(nd, d3(x, y, z), ok2);
     bool ok3;
@@ -1819,9 +1818,8 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
         const D3 nd = unit(direction, ok1);
         const double r1 = rng.next(ovf), r2 = rng.next(ovf);
         const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
-        const double phi = 2.0 * PI * r1;
         double sphi, cphi;
-        k_sincos(phi, &sphi, &cphi);
+        k_sincos_2pi(r1, &sphi, &cphi);  // phi = 2.0 * PI * r1
         const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
         const D3 res = unit(onb_world(nd, d3(x, y, z), ok2), ok3);
         ok = ok1 && ok2 && ok3;
@@ -1845,7 +1843,7 @@ __device__ __forceinline__ D3 mat_tex(const SceneView& S, const DMaterial& M, do
 __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
     double sn, cs;
-    k_sincos(2.0 * PI * r1, &sn, &cs);
+    k_sincos_2pi(r1, &sn, &cs);
     const double s = sqrt(r2 * (1.0 - r2));
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
@@ -2052,7 +2050,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 if constexpr (!HOIST) {
                     const double r1 = rng.next(ovf);
                     r2 = rng.next(ovf);
-                    k_sincos(2.0 * PI * r1, &sn, &cs);
+                    k_sincos_2pi(r1, &sn, &cs);
                 }
                 const double sr2 = sqrt(r2);
                 dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
@@ -2483,7 +2481,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             if (cam) rng.sample = (sie & 0xFFFFu) * F.S + s_j;
             Draws Dr;
             rng.pair(cam ? 0u : vertex, (cam && F.defocus) ? 1u : 0u, Dr.xi0, Dr.xi1);
-            k_sincos(2.0 * PI * Dr.xi0, &Dr.sn, &Dr.cs);
+            k_sincos_2pi(Dr.xi0, &Dr.sn, &Dr.cs);
             RT_DIAG_ONLY(const unsigned long long t_d = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_d - t_b1;
                          dg.cyc_draws += t_d - t_q;)
             if (!cam) {
@@ -2621,10 +2619,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
             D3 origin = F.center;
             if (F.defocus) {
-                const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
+                const double xt = rng.next(ovf);  // theta = 0.0 + (2.0 * PI - 0.0) * xt = 2.0 * PI * xt (vec3.rs:63-69)
                 const double rr = sqrt(rng.next(ovf));
                 double sn, cs;
-                k_sincos(theta, &sn, &cs);
+                k_sincos_2pi(xt, &sn, &cs);
                 origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
             }
             ray.o = origin;
@@ -2725,7 +2723,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 uint32_t ovf = 0;
                 Dr.xi0 = rng.next(ovf);
                 Dr.xi1 = rng.next(ovf);
-                k_sincos(2.0 * PI * Dr.xi0, &Dr.sn, &Dr.cs);
+                k_sincos_2pi(Dr.xi0, &Dr.sn, &Dr.cs);
             }
         }
         bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic, Dr);
@@ -3098,10 +3096,10 @@ __global__ void __launch_bounds__(RT_BLOCK, RT_WF_SHADE_WAVES) rt_wf_shade(const
         const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
         D3 origin = F.center;
         if (F.defocus) {
-            const double theta = 0.0 + (2.0 * PI - 0.0) * rng.next(ovf);  // vec3.rs:63-69
+            const double xt = rng.next(ovf);  // theta = 0.0 + (2.0 * PI - 0.0) * xt = 2.0 * PI * xt (vec3.rs:63-69)
             const double rr = sqrt(rng.next(ovf));
             double sn, cs;
-            k_sincos(theta, &sn, &cs);
+            k_sincos_2pi(xt, &sn, &cs);
             origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
         }
         ray.o = origin;
@@ -3366,6 +3364,8 @@ __global__ void __launch_bounds__(256) rt_math_kernel(int fn, int impl, const do
             case 4: r = rtcr::log(x); break;
             case 5: r = rtcr::acos(x); break;
             case 6: r = rtcr::atan2(x, y); break;
+            case 8: rtcr::sincos_2pi(x, &s, &c), r = s; break;
+            case 9: rtcr::sincos_2pi(x, &s, &c), r = c; break;
             default: r = sqrt(x); break;
         }
     } else {
@@ -3377,6 +3377,8 @@ __global__ void __launch_bounds__(256) rt_math_kernel(int fn, int impl, const do
             case 4: r = ::log(x); break;
             case 5: r = ::acos(x); break;
             case 6: r = ::atan2(x, y); break;
+            case 8: ::sincos(2.0 * PI * x, &s, &c), r = s; break;
+            case 9: ::sincos(2.0 * PI * x, &s, &c), r = c; break;
             default: r = ::sqrt(x); break;
         }
     }

@@ -64,6 +64,18 @@ __device__ __forceinline__ void k_sincos(double x, double* s, double* c) {
     else
         ::sincos(x, s, c);
 }
+// sin / cos of 2.0 * PI * xi for a unit draw xi (every sincos of the path):
+// the same doubles as k_sincos(2.0 * PI * xi), the argument's range known
+// (rtcr::sincos_2pi); RT_SC2PI=0 evaluates k_sincos (A/B only)
+#ifndef RT_SC2PI
+#define RT_SC2PI 1
+#endif
+__device__ __forceinline__ void k_sincos_2pi(double xi, double* s, double* c) {
+    if (RT_CRMATH && RT_SC2PI)
+        rtcr::sincos_2pi(xi, s, c);
+    else
+        k_sincos(2.0 * PI * xi, s, c);
+}
 
 // ---------------------------------------------------------------- RNG
 __device__ __forceinline__ void philox4x32_10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,

@@ -1136,7 +1136,7 @@ int32_t rt_to_rgb_device(const float* lin_dev, uint8_t* srgb_dev, uint64_t n_val
 }
 
 int32_t rt_math_selftest(int32_t fn, int32_t impl, const double* a, const double* b, double* out, uint64_t n) {
-    if (fn < 0 || fn > 7 || impl < 0 || impl > 1) return set_error(RT_EINVAL, "unknown function or implementation");
+    if (fn < 0 || fn > 9 || impl < 0 || impl > 1) return set_error(RT_EINVAL, "unknown function or implementation");
     if (n && (!a || !out || (fn == 6 && !b))) return set_error(RT_EINVAL, "null argument");
     if (n == 0) return RT_OK;
     int dev = 0;

@@ -112,6 +112,30 @@ int main(int argc, char** argv) {
         run(fam((std::string("sincos.cos/") + s.n).c_str()), *s.v, none, sc_c, cos_g, cos_q);
     }
 
+    // ---- sincos_2pi(xi) = sincos(2 pi xi): the path's draws, and xi stepped
+    // ulp by ulp around k / 256 (x next to k pi/128, every k of the range)
+    auto s2_s = [](double xi, double) { double s, c; rtcr::sincos_2pi(xi, &s, &c); return s; };
+    auto s2_c = [](double xi, double) { double s, c; rtcr::sincos_2pi(xi, &s, &c); return c; };
+    auto s2_sg = [PI](double xi, double) { return sin(2.0 * PI * xi); };
+    auto s2_cg = [PI](double xi, double) { return cos(2.0 * PI * xi); };
+    auto s2_sq = [PI](double xi, double) { return (double)sinq((__float128)(2.0 * PI * xi)); };
+    auto s2_cq = [PI](double xi, double) { return (double)cosq((__float128)(2.0 * PI * xi)); };
+    std::vector<double> x_path, x_hard;
+    for (long i = 0; i < N; ++i) x_path.push_back(u01());
+    for (double v : {0.0, 1.0, 0.5, 0.25, 0.75, 0x1p-53, 1.0 - 0x1p-53, 0.125}) x_path.push_back(v);
+    for (int k = 0; k <= 256; ++k) {
+        const double c = k / 256.0;
+        for (int st = -40; st <= 40; ++st) {
+            double xi = c;
+            for (int j = 0; j < (st < 0 ? -st : st); ++j) xi = nextafter(xi, st < 0 ? -1.0 : 2.0);
+            if (xi >= 0.0 && xi <= 1.0) x_hard.push_back(xi);
+        }
+    }
+    run(fam("sincos_2pi.sin/path_xi"), x_path, none, s2_s, s2_sg, s2_sq);
+    run(fam("sincos_2pi.cos/path_xi"), x_path, none, s2_c, s2_cg, s2_cq);
+    run(fam("sincos_2pi.sin/near_k_over_256"), x_hard, none, s2_s, s2_sg, s2_sq);
+    run(fam("sincos_2pi.cos/near_k_over_256"), x_hard, none, s2_c, s2_cg, s2_cq);
+
     // ---- log: the media's ln xi, wide, near 1, subnormal, specials
     auto log_c = [](double x, double) { return rtcr::log(x); };
     auto log_g = [](double x, double) { return log(x); };

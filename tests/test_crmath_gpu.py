@@ -90,3 +90,31 @@ def test_device_math_specials(gpu):
     ours = _eval(gpu, 6, 0, np.ascontiguousarray(ys[0]), np.ascontiguousarray(ys[1]))
     want = np.array([f(y, x) for y, x in zip(*ys)])
     assert (np.signbit(ours) == np.signbit(want)).all() and (ours == want).all()
+
+
+def test_device_sincos_2pi_matches_sincos(gpu):
+    """rtcr::sincos_2pi(xi) -- what every sincos of the kernel calls, the
+    argument 2.0 * PI * xi formed inside -- returns the same doubles as
+    rtcr::sincos(2.0 * PI * xi) (pinned above against the correctly rounded
+    values) on the path's draws and on xi stepped ulp by ulp around every
+    k / 256 (x next to each k pi/128 of its reduction), 0 and 1."""
+    rng = np.random.default_rng(2025)
+    xi = [(rng.integers(0, 1 << 53, 200000, dtype=np.int64) * 2.0 ** -53)]
+    near = []
+    for k in range(257):
+        c = k / 256.0
+        lo = hi = c
+        near.append(c)
+        for _ in range(24):
+            lo, hi = np.nextafter(lo, -1.0), np.nextafter(hi, 2.0)
+            if lo >= 0.0:
+                near.append(lo)
+            if hi <= 1.0:
+                near.append(hi)
+    xi.append(np.array(near + [0.0, 1.0, 2.0 ** -53, 1.0 - 2.0 ** -53]))
+    xi = np.ascontiguousarray(np.concatenate(xi))
+    x = 2.0 * np.pi * xi  # the same double as the kernel's 2.0 * PI * xi
+    for fn2, fn in ((8, 2), (9, 3)):
+        got, want = _eval(gpu, fn2, 0, xi, xi), _eval(gpu, fn, 0, x, x)
+        diff = got != want
+        assert not diff.any(), (fn2, int(diff.sum()), float(xi[np.argmax(diff)]).hex())
