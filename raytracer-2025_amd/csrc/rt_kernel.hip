@@ -1331,6 +1331,9 @@ __device__ __forceinline__ Node4Rows load_node4(const RT_LDS float4* nl, uint32_
     const RT_LDS float4* np = nl + idx * 7u;
     return Node4Rows{np[0], np[1], np[2], np[3], np[4], np[5], np[6]};
 }
+#ifndef RT_SPHERE_RINV
+#define RT_SPHERE_RINV 1  // basic / mesh tiers: a static sphere's 1.0 / r from the flatten, not divided per hit
+#endif
 #ifndef RT_SORT_SKIP
 #define RT_SORT_SKIP 1
 #endif
@@ -1572,19 +1575,21 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
     D3 outward;
     if (!PLANAR || kind == K_SPHERE || kind == K_MSPHERE) {
         D3 c;
-        double radius;
+        double rinv;  // sphere.rs:99: (p - c) / radius = (1.0 / radius) * (p - c) (vec3.rs:225-227)
         if (!FULL || kind == K_SPHERE) {
             const double4 s = S.spheres[idx];
             c = d3(s.x, s.y, s.z);
-            radius = s.w;
+            // basic / mesh tiers: the host's 1.0 / r, the same double (C2 -0.5 %);
+            // the full tiers divide (C5 +1.0 % with the load: A/B, RMSE 0)
+            rinv = (RT_SPHERE_RINV && !FULL) ? S.sphere_rinv[idx] : 1.0 / s.w;
             rec.mat = S.sphere_mat[idx];
         } else {
             const double4 s = S.msph_center[idx], m = S.msph_dir[idx];
             c = d3(s.x, s.y, s.z) + r.time * d3(m.x, m.y, m.z);
-            radius = s.w;
+            rinv = 1.0 / s.w;
             rec.mat = S.msph_mat[idx];
         }
-        outward = divs(p - c, radius);  // sphere.rs:99
+        outward = rinv * (p - c);
         if (S.materials[rec.mat].flags & MF_NEEDS_UV) {
             // sphere.rs:53-61
             const double theta = k_acos(-outward.y);

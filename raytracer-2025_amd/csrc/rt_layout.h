@@ -213,6 +213,7 @@ struct SceneView {
     const RT_GLOBAL DNode4* nodes4;          // 4-wide nodes: K_BVH refs index these
     const RT_GLOBAL double4* spheres;        // {cx, cy, cz, r}
     const RT_GLOBAL int32_t* sphere_mat;
+    const RT_GLOBAL double* sphere_rinv;     // 1.0 / r, rounded as the kernel's division would
     const RT_GLOBAL double4* msph_center;    // moving: {c1.x, c1.y, c1.z, r}
     const RT_GLOBAL double4* msph_dir;       // {c2-c1, 0}
     const RT_GLOBAL int32_t* msph_mat;

@@ -363,6 +363,7 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.nodes4 = (const rtk::DNode4*)off(put(blob, hw.nodes4));
     v.spheres = (const double4*)off(put(blob, hw.spheres));
     v.sphere_mat = (const int32_t*)off(put(blob, hw.sphere_mat));
+    v.sphere_rinv = (const double*)off(put(blob, hw.sphere_rinv));
     v.msph_center = (const double4*)off(put(blob, hw.msph_center));
     v.msph_dir = (const double4*)off(put(blob, hw.msph_dir));
     v.msph_mat = (const int32_t*)off(put(blob, hw.msph_mat));
@@ -495,7 +496,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     char* b = d->blob;
     rtk::SceneView v = fw.rel;
     auto fix = [b](auto& p) { p = reinterpret_cast<std::remove_reference_t<decltype(p)>>(b + (uintptr_t)p); };
-    fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.msph_center), fix(v.msph_dir),
+    fix(v.nodes), fix(v.nodes4), fix(v.spheres), fix(v.sphere_mat), fix(v.sphere_rinv), fix(v.msph_center), fix(v.msph_dir),
         fix(v.msph_mat), fix(v.planars), fix(v.planars_f), fix(v.planar_area), fix(v.planar_mat), fix(v.planar_remap), fix(v.remaps),
         fix(v.remap_nm), fix(v.list_children), fix(v.list_boxes), fix(v.xforms), fix(v.media), fix(v.materials), fix(v.textures),
         fix(v.texels), fix(v.perlin);
@@ -1059,7 +1060,8 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
         int32_t rc = flatten(s, world, lights, bg, (flags & RT_FLAG_REFERENCE_BVH) != 0, hw);
         if (rc != RT_OK) return rc;
         std::vector<char> blob;
-        put(blob, hw.nodes), put(blob, hw.spheres), put(blob, hw.sphere_mat), put(blob, hw.msph_center),
+        put(blob, hw.nodes), put(blob, hw.spheres), put(blob, hw.sphere_mat), put(blob, hw.sphere_rinv),
+            put(blob, hw.msph_center),
             put(blob, hw.msph_dir), put(blob, hw.msph_mat), put(blob, hw.planars), put(blob, hw.planar_area),
             put(blob, hw.planar_mat), put(blob, hw.list_children), put(blob, hw.xforms), put(blob, hw.media),
             put(blob, hw.materials), put(blob, hw.textures), put(blob, hw.texels), put(blob, hw.perlin);

@@ -618,6 +618,7 @@ struct Flattener {
                 uint32_t idx = (uint32_t)out.spheres.size();
                 out.spheres.push_back(make_double4(o.c1.x, o.c1.y, o.c1.z, o.radius));
                 out.sphere_mat.push_back(o.mat);
+                out.sphere_rinv.push_back(1.0 / o.radius);  // vec3.rs:225-227: v / r = (1.0 / r) * v
                 r = {rtk::make_ref(rtk::K_SPHERE, idx), 0};
                 ++out.n_prims;
                 break;

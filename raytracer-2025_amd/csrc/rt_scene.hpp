@@ -110,6 +110,7 @@ struct HostWorld {
     std::vector<rtk::DNode4> nodes4;  // basic tier (bvh4_basic); mesh / full tiers before bvh4_quantize
     std::vector<double4> spheres;
     std::vector<int32_t> sphere_mat;
+    std::vector<double> sphere_rinv;  // 1.0 / radius, the factor of sphere.rs:99's (p - c) / radius
     std::vector<double4> msph_center, msph_dir;
     std::vector<int32_t> msph_mat;
     std::vector<rtk::DPlanar> planars;
