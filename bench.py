@@ -231,8 +231,12 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     `row_stride`-th row of the frame at `spp` (sqrt_spp^2 strata); per-sample
     cost does not depend on spp.  For C2 also BASELINE configs[0] in full
     (book-1 random spheres 400x225, 100 spp), as BASELINE.md plans."""
-    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
-    if not os.path.exists(so):
+    # the timed build: -O3 (cargo --release's opt-level), no work counters
+    # (oracle/Makefile liboracle_fast.so); the counting build the tests and
+    # scripts/work_counts.py use is timed once beside it on the same sample
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_fast.so")
+    so_counting = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not (os.path.exists(so) and os.path.exists(so_counting)):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
     capi = importlib.import_module(PKG + ".capi")
     rt = importlib.import_module(PKG + ".raytracer")
@@ -241,6 +245,10 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     scene = rt.Scene(api)
     world, lights, cam, desc = build_workload(scenes, scene, workload, WORKLOADS[workload][0], spp)
     samples, dt = _oracle_render(api, capi, scene, world, lights, cam, row_stride, threads)
+    api_c = capi.Api(ctypes.CDLL(so_counting), "orc_", capi.ORACLE_EXTRAS)
+    scene_c = rt.Scene(api_c)
+    world_c, lights_c, cam_c, _ = build_workload(scenes, scene_c, workload, WORKLOADS[workload][0], spp)
+    samples_c, dt_c = _oracle_render(api_c, capi, scene_c, world_c, lights_c, cam_c, row_stride, threads)
     # one thread on a proportionally sparser sample: the per-core rate
     samples1, dt1 = _oracle_render(api, capi, scene, world, lights, cam, row_stride * max(1, threads), 1)
     info = cpu_info or {}
@@ -250,6 +258,7 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
+        "build": "oracle/_build/liboracle_fast.so (g++ -O3 -ffp-contract=off, work counters compiled out)",
         "sample": f"{desc.split(':')[0]} scene, every {row_stride}th row of {cam.image_width}x{cam.image_height} at {spp} spp ({cam.sqrt_spp**2} traced), "
                   f"{samples} samples in {dt:.1f} s on {threads} threads of '{cpu_model()}' "
                   f"(all CPUs this job may use: affinity {info.get('affinity')}, cgroup quota {info.get('cgroup_quota')}, "
@@ -259,6 +268,11 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
     res["per_core"] = {"value": per_core, "unit": "Msamples/s", "seconds": round(dt1, 2), "samples": samples1,
                        "sample": f"1 thread, every {row_stride * max(1, threads)}th row at {spp} spp"}
     res["host"] = topo
+    rc = samples_c / dt_c / 1e6
+    res["counting_build"] = {"value": round(rc, 4), "unit": "Msamples/s", "seconds": round(dt_c, 2),
+                             "timed_over_counting": round(res["value"] / rc, 4),
+                             "build": "oracle/_build/liboracle.so (-O2, thread-local work counters: the tests' and "
+                                      "scripts/work_counts.py's build; not the baseline)"}
     # the whole host (every physical core, both hardware threads), ESTIMATED
     # from the measured SMT rate per core: k cores, two threads each, on the
     # same rows as the measured baseline (per-row cost varies: sky rows are

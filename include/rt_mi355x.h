@@ -73,9 +73,12 @@ int32_t rt_tex_image(rt_scene* s, uint32_t width, uint32_t height, const float* 
  * the format comes from the extension as ImageReader::open takes it; the
  * library decodes PNG, JPEG and Radiance HDR (rt_image.hpp: the image crate's
  * into_rgba32f, then the sRGB EOTF unless raw or HDR, image.rs:63-82).  A file
- * that is missing, has no image extension or fails to decode is the
- * reference's Image::EMPTY (cyan); another image format (GIF, EXR, ...) or a
- * CMYK / arithmetic-coded / 12-bit JPEG is RT_EUNSUPPORTED.  raw != 0: no sRGB
+ * that is missing, has no image extension, fails to decode or whose decoded
+ * buffer would pass the image crate's default 512 MiB allocation limit
+ * (ImageReader::decode reserves it first) is the reference's Image::EMPTY
+ * (cyan); another image format (GIF, EXR, ...), a CMYK / arithmetic-coded /
+ * 12-bit JPEG, or a file within the crate's limit but past this library's
+ * 2^28 pixels is RT_EUNSUPPORTED.  raw != 0: no sRGB
  * conversion (new_raw_image); linear_interp selects ImageInterpMethod::Linear. */
 int32_t rt_tex_image_file(rt_scene* s, const char* path, int32_t raw, int32_t linear_interp);
 /* NoiseTexture::new (texture.rs:183-188).  Perlin tables are drawn from

@@ -113,7 +113,7 @@ double Perlin::turb(const Point3& p, int depth) const {
 // ---------------------------------------------------------------- PDFs
 // pdf.rs:77-87
 std::pair<Color, double> HittablePDF::value(const Vec3& direction) const {
-    ++work().light_pdf;
+    ORC_COUNT(light_pdf);
     return {Color(), objects->pdf_value(origin, direction)};
 }
 std::optional<Vec3> HittablePDF::generate() const { return objects->random(origin); }
@@ -187,7 +187,7 @@ std::unique_ptr<BVH> BVH::from_vec(std::vector<HittablePtr> objects) {
 }
 // bvh.rs:57-85
 std::optional<HitRecord> BVH::hit(const Ray& r, const Interval& interval) const {
-    ++work().bvh_node_tests;
+    ORC_COUNT(bvh_node_tests);
     if (!bbox.hit(r, interval)) return std::nullopt;
     std::optional<HitRecord> hit_left;
     double closest_so_far = interval.max;
@@ -224,7 +224,7 @@ void Sphere::get_sphere_uv(const Vec3& p, double& u, double& v) {
 }
 // sphere.rs:77-108
 std::optional<HitRecord> Sphere::hit(const Ray& r, const Interval& interval) const {
-    ++work().sphere_tests;
+    ORC_COUNT(sphere_tests);
     Point3 current_center = center.at(r.time);
     Vec3 oc = current_center - r.orig;
     double a = r.dir.length_squared();
@@ -232,14 +232,14 @@ std::optional<HitRecord> Sphere::hit(const Ray& r, const Interval& interval) con
     double c = oc.length_squared() - radius * radius;
     double discriminant = h * h - a * c;
     if (discriminant < 0.0) return std::nullopt;
-    ++work().sphere_disc_ok;
+    ORC_COUNT(sphere_disc_ok);
     double sqrtd = std::sqrt(discriminant);
     double root = (h - sqrtd) / a;
     if (!interval.contains(root)) {
         root = (h + sqrtd) / a;
         if (!interval.contains(root)) return std::nullopt;
     }
-    ++work().sphere_records;
+    ORC_COUNT(sphere_records);
     Point3 p = r.at(root);
     Vec3 outward_normal = (p - current_center) / radius;
     double u, v;
@@ -313,9 +313,9 @@ std::unique_ptr<Planar> make_triangle(const Point3& a, const Vec3& u, const Vec3
 // quad.rs:71-102 / triangle.rs:69-98
 std::optional<HitRecord> Planar::hit(const Ray& r, const Interval& interval) const {
     if (triangle)
-        ++work().tri_tests;
+        ORC_COUNT(tri_tests);
     else
-        ++work().quad_tests;
+        ORC_COUNT(quad_tests);
     double denom = normal.dot(r.dir);
     if (std::fabs(denom) < 1e-8) return std::nullopt;
     double t = (parm_d - normal.dot(r.orig)) / denom;
@@ -330,7 +330,7 @@ std::optional<HitRecord> Planar::hit(const Ray& r, const Interval& interval) con
     } else {  // quad.rs:57-67
         if (!unit.contains(alpha) || !unit.contains(beta)) return std::nullopt;
     }
-    ++work().planar_records;
+    ORC_COUNT(planar_records);
     return HitRecord::make(intersection, normal, mat.get(), t, alpha, beta, r);
 }
 // quad.rs:108-120 / triangle.rs:108-120
@@ -383,7 +383,7 @@ Transform::Transform(HittablePtr o, const Vec3& off, const Quaternion& q, const 
 }
 // shapes.rs:87-111
 std::optional<HitRecord> Transform::hit(const Ray& r, const Interval& interval) const {
-    ++work().transform_tests;
+    ORC_COUNT(transform_tests);
     Point3 to = r.at(1.0);
     Point3 lo = detransform(r.orig);
     Point3 lt = detransform(to);
@@ -412,7 +412,7 @@ Vec3 Transform::random(const Point3& o) const {
 // ---------------------------------------------------------------- ConstantMedium
 // volume.rs:37-73
 std::optional<HitRecord> ConstantMedium::hit(const Ray& r, const Interval& interval) const {
-    ++work().medium_tests;
+    ORC_COUNT(medium_tests);
     auto rec1 = boundary->hit(r, Interval::universe());
     if (!rec1) return std::nullopt;
     auto rec2 = boundary->hit(r, Interval::make(rec1->t + 0.0001, INF));
@@ -461,7 +461,7 @@ void Camera::initialize() {
 }
 // camera.rs:247-273
 Ray Camera::get_ray(uint32_t i, uint32_t j, uint32_t s_i, uint32_t s_j) const {
-    ++work().camera_rays;
+    ORC_COUNT(camera_rays);
     double px = (((double)s_i + Random::f64()) * recip_sqrt_spp) - 0.5;
     double py = (((double)s_j + Random::f64()) * recip_sqrt_spp) - 0.5;
     Point3 pixel_sample = pixel00_loc + (((double)i + px) * pixel_delta_u) + (((double)j + py) * pixel_delta_v);
@@ -489,14 +489,14 @@ Color Camera::background_value(const Ray& r) const {
 // camera.rs:275-325
 Color Camera::ray_color(const Ray& r, uint32_t depth, const Hittable& world, const Hittable* lights) const {
     if (depth == 0) return Color();
-    ++work().ray_color_calls;
+    ORC_COUNT(ray_color_calls);
     current_rng()->begin_vertex(max_depth - depth + 1);
     auto rec = world.hit(r, Interval::range(1e-8, INF));
     if (!rec) {
-        ++work().sky_miss;
+        ORC_COUNT(sky_miss);
         return background_value(r);
     }
-    ++work().emitted;
+    ORC_COUNT(emitted);
     Color color_from_emission = rec->mat->emitted(r, *rec);
     auto sr = rec->mat->scatter(r, *rec);
     if (!sr) return color_from_emission;

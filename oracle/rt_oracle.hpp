@@ -340,6 +340,15 @@ struct WorkCounts {
     }
 };
 WorkCounts& work();
+// The counting build (liboracle.so: scripts/work_counts.py, the tests) bumps a
+// thread-local counter at every node test, primitive test and scatter; the
+// timed CPU baseline (liboracle_fast.so, bench.py's cpu_baseline) is built
+// with -DORC_NO_COUNTS, so none of those TLS accesses is in the measured work.
+#ifdef ORC_NO_COUNTS
+#define ORC_COUNT(field) ((void)0)
+#else
+#define ORC_COUNT(field) (++::orc::work().field)
+#endif
 
 // ---------------------------------------------------------------- Textures
 // src/texture.rs:5-7
@@ -550,7 +559,7 @@ struct Lambertian : Material {  // material.rs:49-66
     std::shared_ptr<Texture> texture;
     explicit Lambertian(std::shared_ptr<Texture> t) : texture(std::move(t)) {}
     std::optional<ScatterRecord> scatter(const Ray&, const HitRecord& rec) const override {
-        ++work().lambert;
+        ORC_COUNT(lambert);
         Color albedo = texture->value(rec.u, rec.v, rec.p);
         return pdf_record(std::make_unique<CosinePDF>(albedo, rec.normal));
     }
@@ -560,7 +569,7 @@ struct Metal : Material {  // material.rs:68-95
     double fuzz;
     Metal(const Color& a, double f) : albedo(a), fuzz(std::clamp(f, 0.0, 1.0)) {}
     std::optional<ScatterRecord> scatter(const Ray& r_in, const HitRecord& rec) const override {
-        ++work().metal;
+        ORC_COUNT(metal);
         auto ud = from_vec3(r_in.dir);
         if (!ud) return std::nullopt;
         Vec3 raw_reflected = ud->reflect(rec.normal);
@@ -583,7 +592,7 @@ struct Dielectric : Material {  // material.rs:97-144
         return r0sq + (1.0 - r0sq) * x5;
     }
     std::optional<ScatterRecord> scatter(const Ray& r_in, const HitRecord& rec) const override {
-        ++work().dielectric;
+        ORC_COUNT(dielectric);
         double ri = rec.front_face ? 1.0 / refraction_index : refraction_index;
         Vec3 ud = expect_unit(r_in.dir, "Dielectric unwrap");
         double cos_theta = std::fmin((-ud).dot(rec.normal), 1.0);
@@ -619,7 +628,7 @@ struct Isotropic : Material {  // material.rs:188-207
     std::shared_ptr<Texture> texture;
     explicit Isotropic(std::shared_ptr<Texture> t) : texture(std::move(t)) {}
     std::optional<ScatterRecord> scatter(const Ray&, const HitRecord& rec) const override {
-        ++work().isotropic;
+        ORC_COUNT(isotropic);
         Color albedo = texture->value(rec.u, rec.v, rec.p);
         return pdf_record(std::make_unique<SpherePDF>(albedo));
     }

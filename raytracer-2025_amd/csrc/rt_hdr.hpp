@@ -62,6 +62,12 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
         err = "HDR orientation other than -Y h +X w";
         return CORRUPT;
     }
+    // the crate's HDR decoder yields Rgb32F (12 B/px), reserved against its
+    // default 512 MiB limit before decoding: larger fails (-> Image::EMPTY)
+    if ((uint64_t)h * (uint64_t)w * 12 > (512ull << 20)) {
+        err = "HDR's decoded buffer exceeds the image crate's default 512 MiB allocation limit";
+        return CORRUPT;
+    }
     if ((uint64_t)h * (uint64_t)w > (1ull << 28)) {
         err = "HDR larger than this library's 2^28-pixel limit";
         return UNSUPPORTED;

@@ -60,10 +60,12 @@ inline Status load(const std::string& path, bool raw, uint32_t& W, uint32_t& H, 
     while ((n = std::fread(buf, 1, sizeof buf, fp)) > 0) f.insert(f.end(), buf, buf + n);
     std::fclose(fp);
     // Each decoder returns 3 (UNSUPPORTED) for what this library does not
-    // decode -- a library limit (more than 2^28 pixels) or a coding process
-    // it leaves out -- which the crate might decode: RT_EUNSUPPORTED, never a
-    // cyan image; anything else that fails (a bad signature, a corrupt
-    // stream) is the crate's decode error -> Image::EMPTY.
+    // decode -- a library limit (more than 2^28 pixels within the crate's
+    // 512 MiB allocation limit) or a coding process it leaves out -- which
+    // the crate might decode: RT_EUNSUPPORTED, never a cyan image; anything
+    // else that fails (a bad signature, a corrupt stream, a decoded buffer
+    // past the crate's 512 MiB default limit) is the crate's decode error ->
+    // Image::EMPTY.
     int st;
     if (fmt == F_PNG)
         st = (int)rtpng::decode(f, W, H, rgba, err);

@@ -267,6 +267,10 @@ struct Decoder {
         W = be16(p + 3);
         const int nc = p[5];
         if (W == 0 || H == 0) return fail(UNSUPPORTED, "JPEG without its height in the frame header (DNL)");
+        // the crate decodes to L8 (gray) or Rgb8, reserved against its
+        // default 512 MiB limit before decoding: larger fails (-> Image::EMPTY)
+        if ((uint64_t)W * H * (nc == 1 ? 1 : 3) > (512ull << 20))
+            return fail(CORRUPT, "JPEG's decoded buffer exceeds the image crate's default 512 MiB allocation limit");
         if ((uint64_t)W * H > (1ull << 28)) return fail(UNSUPPORTED, "JPEG larger than 2^28 pixels");
         if (nc != 1 && nc != 3) return fail(UNSUPPORTED, "JPEG with other than 1 or 3 components (CMYK / YCCK)");
         if (len < 6 + 3 * (size_t)nc) return fail(CORRUPT, "short SOF");

@@ -25,6 +25,10 @@ namespace rtpng {
 
 enum Status { OK = 0, MISSING = 1, CORRUPT = 2, UNSUPPORTED = 3 };
 
+// image 0.25 Limits::default().max_alloc (512 MiB): ImageReader::decode fails
+// on an image whose decoded buffer is larger (limits.reserve(total_bytes))
+constexpr uint64_t CRATE_MAX_ALLOC = 512ull << 20;
+
 inline uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
 // palette 0.7 Srgb -> LinSrgb for f32 components (the IEC 61966-2-1 EOTF)
@@ -94,6 +98,18 @@ inline Status decode(const std::vector<uint8_t>& f, uint32_t& W, uint32_t& H, st
     if (!depth_ok || (ctype == 3 && plte.empty())) {
         err = "bad PNG bit depth / palette";
         return CORRUPT;
+    }
+    // image 0.25's ImageReader::decode reserves the decoded buffer against
+    // its default Limits (max_alloc 512 MiB) before decoding: a larger image
+    // fails to decode there (-> Image::EMPTY, utils/image.rs:50-52).  Its PNG
+    // decoder expands palettes to RGB, low bit depths to 8 and tRNS to an
+    // alpha channel, and keeps 16-bit samples 16-bit.
+    {
+        const uint64_t out_ch = (ctype == 3 ? 3 : channels) + ((!trns.empty() && (ctype == 0 || ctype == 2 || ctype == 3)) ? 1 : 0);
+        if ((uint64_t)W * H * out_ch * (depth == 16 ? 2 : 1) > CRATE_MAX_ALLOC) {
+            err = "PNG's decoded buffer exceeds the image crate's default 512 MiB allocation limit";
+            return CORRUPT;
+        }
     }
     if ((uint64_t)W * H > (1ull << 28)) {
         err = "PNG larger than this library's 2^28-pixel limit";

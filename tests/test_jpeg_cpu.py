@@ -288,21 +288,41 @@ def test_jpeg_malformed_huffman_tables(load_asan, tmp_path):
 
 
 def test_png_and_hdr_limits(load_asan, tmp_path):
-    """A file past the library's 2^28-pixel limit is RT_EUNSUPPORTED (3) -- the
-    crate might decode it -- not Image::EMPTY; a bad signature is EMPTY (1)."""
+    """image 0.25's ImageReader::decode reserves the decoded buffer against its
+    default Limits (max_alloc 512 MiB) before decoding, so a larger image is
+    the crate's decode error -> Image::EMPTY (1) (utils/image.rs:50-52), not
+    RT_EUNSUPPORTED; a file within the crate's limit but past this library's
+    2^28-pixel limit (possible only at 1 B/px) is RT_EUNSUPPORTED (3); a bad
+    signature is EMPTY (1)."""
     import struct
     import zlib
 
     def chunk(t, d):
         return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xffffffff)
-    big = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", 1 << 15, 1 << 14, 8, 2, 0, 0, 0)) + \
-        chunk(b"IDAT", zlib.compress(b"\x00" * 16)) + chunk(b"IEND", b"")
+
+    def png(w, h, depth, ctype, trns=b""):
+        return b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0)) + \
+            (chunk(b"tRNS", trns) if trns else b"") + chunk(b"IDAT", zlib.compress(b"\x00" * 16)) + chunk(b"IEND", b"")
+    # 2^29 px of RGB8: 1.5 GiB decoded -> the crate fails -> EMPTY
+    big = png(1 << 15, 1 << 14, 8, 2)
     (tmp_path / "big.png").write_bytes(big)
-    assert load_asan(tmp_path / "big.png", False, tmp_path)[0] == 3
+    assert load_asan(tmp_path / "big.png", False, tmp_path)[0] == 1
+    # 2^28 + 2^14 px of L8: 256 MiB, within the crate's limit, past the library's
+    (tmp_path / "gray.png").write_bytes(png(1 << 14, (1 << 14) + 1, 8, 0))
+    assert load_asan(tmp_path / "gray.png", False, tmp_path)[0] == 3
+    # the same with tRNS: expanded to La8, 512 MiB + 32 KiB -> EMPTY
+    (tmp_path / "grayt.png").write_bytes(png(1 << 14, (1 << 14) + 1, 8, 0, b"\x00\x00"))
+    assert load_asan(tmp_path / "grayt.png", False, tmp_path)[0] == 1
+    # 16-bit RGBA at 8 B/px: 8192 x 8193 is 64 KiB over 512 MiB -> EMPTY
+    (tmp_path / "rgba16.png").write_bytes(png(8192, 8193, 16, 6))
+    assert load_asan(tmp_path / "rgba16.png", False, tmp_path)[0] == 1
     (tmp_path / "sig.png").write_bytes(b"\x89PNX\r\n\x1a\n" + big[8:])
     assert load_asan(tmp_path / "sig.png", False, tmp_path)[0] == 1
+    # HDR decodes to Rgb32F (12 B/px): 2^29 px and 44.8 M px (> 512 MiB) -> EMPTY
     (tmp_path / "big.hdr").write_bytes(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y 32768 +X 16384\n")
-    assert load_asan(tmp_path / "big.hdr", False, tmp_path)[0] == 3
+    assert load_asan(tmp_path / "big.hdr", False, tmp_path)[0] == 1
+    (tmp_path / "mid.hdr").write_bytes(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n-Y 6690 +X 6690\n")
+    assert load_asan(tmp_path / "mid.hdr", False, tmp_path)[0] == 1
 
 
 @pytest.mark.parametrize("chain", [4, 9, 40])

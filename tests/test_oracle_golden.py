@@ -64,3 +64,41 @@ def test_sample_count_and_strata(oracle, rt, scenes):
     world, lights, cam = scenes.random_spheres(scene, 16, 10)
     _, _, st = cam.render(world, lights)
     assert st.samples == 16 * 9 * 9
+
+
+@pytest.fixture(scope="module")
+def oracle_fast(capi, oracle):
+    """liboracle_fast.so: the timed CPU baseline (-O3, work counters compiled
+    out; oracle/Makefile)."""
+    return capi.Api(ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "liboracle_fast.so")), "orc_",
+                    capi.ORACLE_EXTRAS)
+
+
+@pytest.mark.parametrize("name", sorted(gen_golden.CASES))
+def test_timed_baseline_build_renders_the_same_bits(oracle, oracle_fast, name):
+    """bench.py times liboracle_fast.so; it must compute exactly what the
+    counting build the tests check computes (same f64 operations: -O3 changes
+    no rounding under -ffp-contract=off)."""
+    build, seed = gen_golden.CASES[name]
+    a = gen_golden.render(oracle, build, seed)
+    b = gen_golden.render(oracle_fast, build, seed)
+    assert a.dtype == b.dtype and a.shape == b.shape
+    assert a.tobytes() == b.tobytes()
+
+
+def test_timed_baseline_build_has_no_counts(oracle, oracle_fast, rt, scenes):
+    """The counting build reports work per sample; the timed build counts
+    nothing (its render loop carries no thread-local increments)."""
+    n = oracle.work_count_fields()
+    counts = []
+    for api in (oracle, oracle_fast):
+        scene = rt.Scene(api)
+        world, lights, cam = scenes.random_spheres(scene, 16, 4)
+        c = cam.to_c()
+        opts = rt.Camera._opts(api, 1, 0, 1, 0, 0)[0]
+        wc = (ctypes.c_uint64 * n)()
+        api.check(api.render_f64(scene.s, world.h, -1 if lights is None else lights.h, ctypes.byref(c),
+                                 ctypes.byref(opts), None, None, None, wc))
+        counts.append(list(wc))
+    assert sum(counts[0]) > 0
+    assert sum(counts[1]) == 0
