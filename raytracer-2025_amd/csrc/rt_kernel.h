@@ -152,17 +152,7 @@ extern "C" hipError_t rtk_launch_deinterleave_u8(const uint8_t* staging, size_t 
 extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_t n, int toon, hipStream_t stream);
 extern "C" hipError_t rtk_launch_math(int fn, int impl, const double* a, const double* b, double* out, uint64_t n,
                                       hipStream_t stream);
-// The full tier's frame as wavefront bounces (rt_kernel.hip rt_wf_walk /
-// rt_wf_shade) over n_slots path slots: wf_d holds 17 x n_slots doubles, wf_u
-// 19 x n_slots uint32, wf_ctr 2 uint32; stack_ovf sized for walk_grid blocks.
-// Blocks the calling thread every check_every bounces (the end test).
-extern "C" hipError_t rtk_launch_frame_wf(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
-                                          double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
-                                          int toon, hipStream_t stream, int tier, int walk_grid, void* params_dev,
-                                          void* stack_ovf, double* wf_d, uint32_t* wf_u, uint32_t* wf_ctr,
-                                          uint32_t n_slots, uint32_t check_every);
-extern "C" int rtk_wf_walk_occupancy(int* blocks_per_cu);
-// device bytes rtk_launch_frame (and rtk_launch_frame_wf) needs at params_dev
+// device bytes rtk_launch_frame needs at params_dev
 extern "C" size_t rtk_params_bytes(void);
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu);
 // threads per block of a tier's path kernel

@@ -892,25 +892,6 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
     return t <= tmax;
 }
 
-// medium_hit for a medium whose boundary is one-pass (DMedium::planar_n or
-// bsphere: the wavefront shade kernel's media, rt_render.cpp checks)
-__device__ __forceinline__ bool medium_hit_onepass(const SceneView& S, uint32_t idx, const Ray& r, double tmin,
-                                                   double tmax, const Rng& rng, double& t) {
-    const DMedium M = S.media[idx];
-    double t1 = 0.0, t2 = 0.0;
-    if (!boundary_onepass(S, M, r, t1, t2)) return false;
-    if (t1 < tmin) t1 = tmin;
-    if (t2 > tmax) t2 = tmax;
-    if (t1 >= t2) return false;
-    if (t1 < 0.0) t1 = 0.0;
-    const double ray_length = len(r.d);
-    const double inside = (t2 - t1) * ray_length;
-    const double hd = M.neg_inv_density * k_log(rng.medium(M.medium_id));
-    if (hd > inside) return false;
-    t = t1 + hd / ray_length;  // volume.rs:65
-    return t <= tmax;
-}
-
 // world.hit(r, [1e-8, inf)) (camera.rs:286) as a depth-first walk with one
 // running closest t.  Lists are walked in order with the interval shrunk to
 // the best hit so far (hits.rs:34-46 tests every child with the full interval
@@ -1057,12 +1038,9 @@ struct MedQ {
 };
 
 // One stack entry of the walk; false when the walk is over (T.found, T.hit hold the result).
-// INLINE_MEDIA false (the wavefront walk): a medium is only ever queued --
-// the world's media fit the queue (rt_render.cpp) -- and a full queue is
-// counted as a panic rather than tested here.
-template <int TIER, class WR, bool INLINE_MEDIA = true>
+template <int TIER, class WR>
 __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Trav<TIER>& T, StackFor<TIER>& stk,
-                                           const Rng& rng, MedQ med, Diag& dg, uint32_t* overflow = nullptr) {
+                                           const Rng& rng, MedQ med, Diag& dg) {
     const auto wq = world_ray(wrr);
     constexpr bool FULL = tier_full(TIER);
     constexpr double tmin = 1e-8;
@@ -1252,10 +1230,8 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                 if (T.nmed < RT_MEDIA_CAP) {
                     med.set(T.nmed, make_uint4(idx, T.nxf, T.xfs.a, T.xfs.b));
                     ++T.nmed;
-                } else if constexpr (INLINE_MEDIA) {
-                    got = medium_hit<TIER != TIER_FULL_FLAT>(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
                 } else {
-                    ++*overflow;
+                    got = medium_hit<TIER != TIER_FULL_FLAT>(S, idx, r, tmin, T.cl.c, stk, T.sp, rng, t);
                 }
                 break;
             }
@@ -1903,11 +1879,11 @@ __device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p
 // ------------------------------------------------------------------ one ray_color level
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
-template <int TIER, bool PLDS = true>  // PLDS: the block holds the LDS copy of the first Perlin table
+template <int TIER>
 __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
                                       const HitInfo& h, bool& panic, const Draws& Dr = Draws{}) {
     constexpr bool FULL = tier_full(TIER);
-    constexpr bool PL = PLDS && tier_full_bvh(TIER) && RT_PERLIN_LDS;  // the flat tier's LDS is full
+    constexpr bool PL = tier_full_bvh(TIER) && RT_PERLIN_LDS;  // the block holds the LDS copy of the first Perlin table (the flat tier's LDS is full)
     uint32_t ovf = 0;
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
@@ -2835,312 +2811,6 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
 }
 
 
-// ------------------------------------------------------------------ wavefront (full tier)
-// The full tier's megakernel holds a lane's whole path -- walk state, path
-// state and the shading code's temporaries -- in one register budget (246
-// VGPRs, 2 waves per SIMD), and its walks run at 63 % lane efficiency between
-// shading batches.  The wavefront variant (SURVEY §7's fallback for low VALU
-// use; RT_WAVEFRONT=1) keeps each path slot's state in HBM (WfSlots, SoA) and
-// runs a bounce as two kernels over all slots:
-//   rt_wf_walk:  world.hit of every slot's ray (the megakernel's trace_step),
-//                persistent lanes that take new slots in batches as their
-//                walks end; the media a walk meets are queued with the hit
-//                (worlds whose media fit the queue and have one-pass
-//                boundaries: rt_render.cpp checks), so the walk carries no
-//                medium code and fits 4 waves per SIMD;
-//   rt_wf_shade: one thread per slot: the queued media against the walk's
-//                closest t (media_phase), ray_color's level for the hit (the
-//                megakernel's shade code), the sample's end (its sum in s_j
-//                order, the entry's sum to its part-sum slot), the queue
-//                refill and the next sample's camera ray.
-// A slot works through queue entries exactly as a megakernel lane does (the
-// same entries, samples in s_j order, the same RNG keys), so the frame's bits
-// are the megakernel's.
-struct WfSlots {
-    double* d;     // [WF_D][n]: o.xyz, d.xyz, time, beta.xyz, L.xyz, acc.xyz, hit t
-    uint32_t* u;   // [WF_U][n]: q, s_j, sie, pixel, vertex, flags, hit ref, nxf, xf a, xf b, media n, 2 x medium (4)
-    uint32_t* ctr; // [0] the walk kernel's slot counter, [1] live slots (counted when asked)
-    uint32_t n;
-};
-enum : uint32_t { WF_D = 17, WF_U = 19 };
-enum : uint32_t { WF_ALIVE = 1u, WF_PATH = 2u, WF_NEED = 4u };
-struct WfParams {
-    KParams K;
-    WfSlots W;
-};
-#ifndef RT_WF_WALK_WAVES
-#define RT_WF_WALK_WAVES 4
-#endif
-#ifndef RT_WF_SHADE_WAVES
-#define RT_WF_SHADE_WAVES 3
-#endif
-#ifndef RT_WF_REFILL
-#define RT_WF_REFILL 32  // idle lanes of a walk wave that trigger a batch of new slots
-#endif
-#ifndef RT_WF_CHUNK
-#define RT_WF_CHUNK 256  // slots per counter atomic of a walk wave
-#endif
-
-template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, RT_WF_WALK_WAVES) rt_wf_walk(const WfParams* __restrict__ P) {
-    static_assert(TIER == TIER_FULL, "wavefront: the full tier");
-    const SceneView S = P->K.S;
-    const Frame& F = P->K.F;
-    const WfSlots W = P->W;
-    const size_t n = W.n;
-    constexpr int STACK = lds_stack_entries(TIER);
-    __shared__ uint2 lane_lds[(STACK + 2 * RT_MEDIA_CAP) * RT_BLOCK];  // stack rows, then MedQ's
-    RT_LDS uint2* const lrow = (RT_LDS uint2*)(lane_lds + threadIdx.x);
-    const MedQ med{lrow + STACK * RT_BLOCK};
-    StackFor<TIER> stk = make_stack<TIER>(lrow, (RT_LDS uint32_t*)lrow,
-                                          P->K.stack_ovf + (uint64_t)blockIdx.x * RT_BLOCK + threadIdx.x,
-                                          gridDim.x * RT_BLOCK);
-    const uint32_t lane = __lane_id();
-    Rng rng;
-    rng.k0 = F.key0;
-    rng.k1 = F.key1;
-    Diag dg;
-    Trav<TIER> T;
-    Ray ray;
-    uint32_t slot = 0, n_rays = 0, n_overflow = 0;
-    bool walking = false;
-    // the wave's pool of slot indices (wave-uniform)
-    uint32_t pool_next = 0, pool_end = 0;
-    for (;;) {
-        // a batch of new slots for the idle lanes, once RT_WF_REFILL of them
-        // are idle or none walks: trace_begin runs for the batch at once
-        const unsigned long long idle = __ballot(!walking), act = __ballot(true);
-        if ((uint32_t)__popcll(idle) >= RT_WF_REFILL || idle == act) {
-            const uint32_t k = (uint32_t)__popcll(idle);
-            const uint32_t avail = pool_end - pool_next;
-            uint32_t fresh = 0;
-            if (avail < k) {
-                const uint32_t leader = __ffsll((long long)idle) - 1;
-                if (lane == leader) fresh = atomicAdd(&W.ctr[0], (uint32_t)RT_WF_CHUNK);
-                fresh = __shfl(fresh, leader);
-            }
-            const uint32_t old_next = pool_next;
-            if (avail < k) {
-                pool_next = fresh + (k - avail);
-                pool_end = fresh + RT_WF_CHUNK;
-            } else {
-                pool_next += k;
-            }
-            if (!walking) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                slot = rank < avail ? old_next + rank : fresh + (rank - avail);
-                if (slot >= W.n) break;
-                if (W.u[5 * n + slot] & WF_PATH) {
-                    const double* d = W.d + slot;
-                    ray.o = d3(d[0], d[n], d[2 * n]);
-                    ray.d = d3(d[3 * n], d[4 * n], d[5 * n]);
-                    ray.time = d[6 * n];
-                    ++n_rays;
-                    trace_begin<TIER>(S, ray, T);
-                    walking = true;
-                }
-            }
-        }
-        if (!walking) continue;
-        walking = trace_step<TIER, Ray, false>(S, ray, T, stk, rng, med, dg, &n_overflow);
-        if (!walking) {  // the hit and the queued media, for rt_wf_shade
-            W.d[16 * n + slot] = T.hit.t;
-            W.u[6 * n + slot] = T.found ? T.hit.ref : REF_NONE;
-            W.u[7 * n + slot] = T.hit.nxf;
-            W.u[8 * n + slot] = T.hit.xf.a;
-            W.u[9 * n + slot] = T.hit.xf.b;
-            W.u[10 * n + slot] = T.nmed;
-            for (uint32_t k = 0; k < T.nmed; ++k) {
-                const uint4 e = med.get(k);
-                uint32_t* m = W.u + (11 + 4 * k) * n + slot;
-                m[0] = e.x, m[n] = e.y, m[2 * n] = e.z, m[3 * n] = e.w;
-            }
-        }
-    }
-    uint32_t rays_w = n_rays, ovf_w = n_overflow;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) rays_w += __shfl_xor(rays_w, o), ovf_w += __shfl_xor(ovf_w, o);
-    if (lane == 0 && rays_w) atomicAdd(&P->K.stats[0], (unsigned long long)rays_w);
-    if (lane == 0 && ovf_w) atomicAdd(&P->K.stats[1], (unsigned long long)ovf_w);  // cannot happen: fail loudly
-}
-
-// One bounce's shading of every slot (a thread per slot), then each slot's
-// next ray: the same steps as the megakernel's main loop after its walk.
-// count_live: add the slots still alive to ctr[1] (the host's end test).
-template <int TIER>
-__global__ void __launch_bounds__(RT_BLOCK, RT_WF_SHADE_WAVES) rt_wf_shade(const WfParams* __restrict__ P,
-                                                                          int count_live) {
-    const SceneView S = P->K.S;
-    const Frame& F = P->K.F;
-    const WfSlots W = P->W;
-    const uint32_t lane = __lane_id();
-    const uint32_t slot = blockIdx.x * RT_BLOCK + threadIdx.x;
-    if (slot == 0) W.ctr[0] = 0u;  // the next walk's slot counter (this launch follows the last walk)
-    uint32_t fl = slot < W.n ? W.u[5 * W.n + slot] : 0u;
-    const size_t n = W.n;
-    Rng rng;
-    rng.k0 = F.key0;
-    rng.k1 = F.key1;
-    uint32_t n_panics = 0;
-    uint32_t q = 0, s_j = 0, sie = 0, vertex = 0;
-    Ray ray;
-    D3 beta = d3(1, 1, 1), L = d3(0, 0, 0);
-    bool dirty = false;  // the path state changed: store it
-    if (fl & WF_ALIVE) {
-        q = W.u[slot];
-        s_j = W.u[1 * n + slot];
-        sie = W.u[2 * n + slot];
-        rng.pixel = W.u[3 * n + slot];
-        vertex = W.u[4 * n + slot];
-        rng.sample = (sie & 0xFFFFu) * F.S + s_j;
-    }
-    if (fl & WF_PATH) {
-        const double* d = W.d + slot;
-        ray.o = d3(d[0], d[n], d[2 * n]);
-        ray.d = d3(d[3 * n], d[4 * n], d[5 * n]);
-        ray.time = d[6 * n];
-        beta = d3(d[7 * n], d[8 * n], d[9 * n]);
-        L = d3(d[10 * n], d[11 * n], d[12 * n]);
-        HitInfo h;
-        h.t = d[16 * n];
-        h.ref = W.u[6 * n + slot];
-        h.nxf = W.u[7 * n + slot];
-        h.xf.a = W.u[8 * n + slot];
-        h.xf.b = W.u[9 * n + slot];
-        rng.begin(vertex);
-        // the walk's queued media against its closest t (media_phase, volume.rs:37-73)
-        const uint32_t nmed = W.u[10 * n + slot];
-        for (uint32_t k = 0; k < nmed; ++k) {
-            const uint32_t* m = W.u + (11 + 4 * k) * n + slot;
-            const uint32_t mid = m[0], mnxf = m[n], ma = m[2 * n], mb = m[3 * n];
-            Ray r = ray;
-            for (uint32_t j = 0; j < mnxf; ++j) r = xf_ray(S.xforms[j == 0 ? ma : mb], r);
-            double t;
-            const double tmax = h.ref != REF_NONE ? h.t : __builtin_huge_val();
-            if (medium_hit_onepass(S, mid, r, 1e-8, tmax, rng, t)) {
-                h.t = t;
-                h.ref = make_ref(K_MEDIUM, mid);
-                h.nxf = mnxf;
-                h.xf.a = ma;
-                h.xf.b = mb;
-            }
-        }
-        // ---- one ray_color level (camera.rs:275-325) for the hit
-        bool panic = false;
-        bool end_path = shade<TIER, false>(S, ray, beta, L, rng, h.ref != REF_NONE, h, panic);
-        if (panic) {
-            ++n_panics;
-            end_path = true;
-        }
-        if (!end_path) {
-            ++vertex;
-            if (vertex > F.max_depth) end_path = true;  // depth == 0 -> BLACK (camera.rs:282-284)
-        }
-        dirty = true;
-        if (end_path) {
-            if (isnan(L.x) || isnan(L.y) || isnan(L.z)) {  // camera.rs:323
-                ++n_panics;
-                L = d3(0, 0, 0);
-            }
-            double* a = W.d + 13 * n + slot;
-            const D3 acc = d3(a[0], a[n], a[2 * n]) + L;
-            fl &= ~WF_PATH;
-            ++s_j;
-            if (s_j == (sie >> 16)) {
-                double* dst = P->K.partial + (uint64_t)q * 3;
-                dst[0] = acc.x;
-                dst[1] = acc.y;
-                dst[2] = acc.z;
-                fl |= WF_NEED;
-            } else {
-                a[0] = acc.x, a[n] = acc.y, a[2 * n] = acc.z;
-            }
-        }
-    }
-    // ---- refill: the slots that need a queue entry take one each (one
-    // atomic per wave); past the end of the queue a slot is done.  (Pools
-    // of consecutive entries per 64-slot group, as a megakernel wave holds,
-    // made the shading coherent but the frame's end ragged: C5 at 64 spp
-    // 283 -> 351 ms.)
-    const unsigned long long mask = __ballot((fl & WF_NEED) != 0);
-    if (mask) {
-        const uint32_t leader = __ffsll((long long)mask) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(P->K.queue, (uint32_t)__popcll(mask));
-        base = __shfl(base, leader);
-        if (fl & WF_NEED) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            q = base + rank;
-            dirty = true;
-            if (q >= F.queue_total) {
-                fl = 0u;  // no more work for this slot
-            } else {
-                fl &= ~WF_NEED;
-                uint32_t item, s_end;
-                queue_entry(F, q, item, s_j, s_end);
-                const uint32_t pl = udiv_inv(item, F.inv_S), s_i = item - pl * F.S;
-                sie = s_i | (s_end << 16);
-                const uint32_t prow = udiv_inv(pl, F.inv_W);
-                rng.pixel = (F.row_offset + prow * F.row_stride) * F.W + (pl - prow * F.W);
-                double* a = W.d + 13 * n + slot;
-                a[0] = 0.0, a[n] = 0.0, a[2 * n] = 0.0;
-            }
-        }
-    }
-    if ((fl & WF_ALIVE) && !(fl & WF_PATH)) {
-        // ---- Camera::get_ray (camera.rs:247-273), vertex 0, of the next sample
-        const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
-        rng.sample = s_i * F.S + s_j;
-        rng.begin(0);
-        uint32_t ovf = 0;
-        const double xi0 = rng.next(ovf), xi1 = rng.next(ovf);
-        const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
-        const double oy = (((double)s_j + xi1) * F.recip_sqrt_spp) - 0.5;
-        const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
-        D3 origin = F.center;
-        if (F.defocus) {
-            const double xt = rng.next(ovf);  // theta = 0.0 + (2.0 * PI - 0.0) * xt = 2.0 * PI * xt (vec3.rs:63-69)
-            const double rr = sqrt(rng.next(ovf));
-            double sn, cs;
-            k_sincos_2pi(xt, &sn, &cs);
-            origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
-        }
-        ray.o = origin;
-        ray.d = ps - origin;
-        ray.time = rng.next(ovf);
-        beta = d3(1, 1, 1);
-        L = d3(0, 0, 0);
-        vertex = 1;
-        fl |= WF_PATH;
-        dirty = true;
-    }
-    if (dirty) {
-        double* d = W.d + slot;
-        if (fl & WF_PATH) {
-            d[0] = ray.o.x, d[n] = ray.o.y, d[2 * n] = ray.o.z;
-            d[3 * n] = ray.d.x, d[4 * n] = ray.d.y, d[5 * n] = ray.d.z;
-            d[6 * n] = ray.time;
-            d[7 * n] = beta.x, d[8 * n] = beta.y, d[9 * n] = beta.z;
-            d[10 * n] = L.x, d[11 * n] = L.y, d[12 * n] = L.z;
-        }
-        W.u[slot] = q;
-        W.u[1 * n + slot] = s_j;
-        W.u[2 * n + slot] = sie;
-        W.u[3 * n + slot] = rng.pixel;
-        W.u[4 * n + slot] = vertex;
-        W.u[5 * n + slot] = fl;
-    }
-    uint32_t panics_w = n_panics;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) panics_w += __shfl_xor(panics_w, o);
-    if (lane == 0 && panics_w) atomicAdd(&P->K.stats[1], (unsigned long long)panics_w);
-    if (count_live) {
-        const unsigned long long alive = __ballot((fl & WF_ALIVE) != 0);
-        if (lane == 0 && alive) atomicAdd(&W.ctr[1], (uint32_t)__popcll(alive));
-    }
-}
 }  // namespace rtk
 
 // ------------------------------------------------------------------ host launchers
@@ -3166,19 +2836,6 @@ RT_TIER_ENTRY(1)
 #endif
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 2
 RT_TIER_ENTRY(2)
-// the full tier's wavefront kernels (rt_wf_walk / rt_wf_shade)
-extern "C" hipError_t rtk_launch_wf_walk_2(int grid, hipStream_t stream, const rtk::WfParams* P) {
-    hipLaunchKernelGGL(rtk::rt_wf_walk<2>, dim3(grid), dim3(RT_BLOCK), 0, stream, P);
-    return hipGetLastError();
-}
-extern "C" hipError_t rtk_launch_wf_shade_2(uint32_t n_slots, hipStream_t stream, const rtk::WfParams* P, int count_live) {
-    hipLaunchKernelGGL(rtk::rt_wf_shade<2>, dim3((n_slots + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, stream, P,
-                       count_live);
-    return hipGetLastError();
-}
-extern "C" int rtk_wf_walk_occupancy_2(int* blocks_per_cu) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rtk::rt_wf_walk<2>, RT_BLOCK, 0);
-}
 #endif
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 3
 RT_TIER_ENTRY(3)
@@ -3232,9 +2889,6 @@ extern "C" hipError_t rtk_launch_path_2(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_3(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_4(int, hipStream_t, const rtk::KParams*);
 extern "C" int rtk_occupancy_0(int*);
-extern "C" hipError_t rtk_launch_wf_walk_2(int, hipStream_t, const rtk::WfParams*);
-extern "C" hipError_t rtk_launch_wf_shade_2(uint32_t, hipStream_t, const rtk::WfParams*, int);
-extern "C" int rtk_wf_walk_occupancy_2(int*);
 extern "C" int rtk_occupancy_1(int*);
 extern "C" int rtk_occupancy_2(int*);
 extern "C" int rtk_occupancy_3(int*);
@@ -3565,51 +3219,6 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     return launch_reduce(fd, K.F, partial, out, srgb, toon, stream);
 }
 
-// The full tier's frame as wavefront bounces (rt_wf_walk / rt_wf_shade over
-// n_slots path slots, wf_d / wf_u / wf_ctr: WfSlots); the host checks every
-// RT_WF_CHECK bounces whether a slot is still alive, so the call returns
-// when the frame's kernels are all issued and the path work is done.
-extern "C" hipError_t rtk_launch_frame_wf(const rtk::SceneView* view, const rtk_frame_desc* fd, uint32_t* queue,
-                                          double* partial, unsigned long long* stats, float* out, uint8_t* srgb,
-                                          int toon, hipStream_t stream, int tier, int walk_grid, void* params_dev,
-                                          void* stack_ovf, double* wf_d, uint32_t* wf_u, uint32_t* wf_ctr,
-                                          uint32_t n_slots, uint32_t check_every) {
-    if (tier != rtk::TIER_FULL) return hipErrorInvalidValue;
-    rtk::WfParams WP;
-    fill_kparams(WP.K, view, fd, queue, partial, stats, tier, walk_grid, stack_ovf, 0u);
-    WP.W.d = wf_d;
-    WP.W.u = wf_u;
-    WP.W.ctr = wf_ctr;
-    WP.W.n = n_slots;
-    rtk::WfParams* Pd = (rtk::WfParams*)params_dev;
-    hipError_t e = hipMemcpyAsync(Pd, &WP, sizeof WP, hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) return e;
-    if ((e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(wf_ctr, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)(wf_u + 5 * (size_t)n_slots), rtk::WF_ALIVE | rtk::WF_NEED, n_slots,
-                               stream)) != hipSuccess)
-        return e;
-    if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
-    if ((e = rtk_launch_wf_shade_2(n_slots, stream, Pd, 0)) != hipSuccess) return e;  // entries + camera rays
-    if (check_every == 0) check_every = 32;
-    for (uint64_t it = 1;; ++it) {
-        if ((e = rtk_launch_wf_walk_2(walk_grid, stream, Pd)) != hipSuccess) return e;
-        const bool check = it % check_every == 0;
-        if ((e = rtk_launch_wf_shade_2(n_slots, stream, Pd, check ? 1 : 0)) != hipSuccess) return e;
-        if (check) {
-            uint32_t live = 0;
-            if ((e = hipMemcpyAsync(&live, wf_ctr + 1, sizeof live, hipMemcpyDeviceToHost, stream)) != hipSuccess) return e;
-            if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-            if (live == 0) break;
-            if ((e = hipMemsetAsync(wf_ctr + 1, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
-        }
-    }
-    if (fd->ev_stop) (void)hipEventRecord((hipEvent_t)fd->ev_stop, stream);
-    return launch_reduce(fd, WP.K.F, partial, out, srgb, toon, stream);
-}
-
-extern "C" int rtk_wf_walk_occupancy(int* blocks_per_cu) { return rtk_wf_walk_occupancy_2(blocks_per_cu); }
-
 extern "C" hipError_t rtk_launch_deinterleave(const float* staging, size_t slice, float* out, uint32_t rows, uint32_t W,
                                               uint32_t parts, hipStream_t stream) {
     const uint64_t n = (uint64_t)rows * W * 3;
@@ -3703,7 +3312,7 @@ extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row
     return n < rows ? n : rows;
 }
 
-extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::WfParams); }  // (>= sizeof(KParams))
+extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
 
 
 extern "C" int rtk_path_kernel_occupancy(int tier, int* blocks_per_cu) {

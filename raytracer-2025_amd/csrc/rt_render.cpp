@@ -29,6 +29,12 @@
 
 // ---------------------------------------------------------------------------- RCCL
 // librccl is opened on first use (a single-GPU render never loads it).
+// Check build only (make check, -DRT_CHECK): RT_RCCL_LIB names another library
+// with librccl's point-to-point ABI instead -- the test-only stand-in
+// tests/cpp/fake_rccl.cpp, with which one process on one GPU runs the
+// nranks > 1 gathers (tests/test_gather_standin_gpu.py).  The product library
+// reads no such variable: it opens librccl and nothing else.  Each library is
+// opened once; a communicator keeps the API it was made with.
 namespace {
 struct RcclApi {
     bool ok = false;
@@ -45,40 +51,56 @@ struct RcclApi {
 };
 
 RcclApi& rccl() {
-    static RcclApi a;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    static std::mutex m;
+    static std::map<std::string, RcclApi*>* apis = new std::map<std::string, RcclApi*>();  // never freed
+#ifdef RT_CHECK
+    const char* env = std::getenv("RT_RCCL_LIB");
+    const std::string path = env ? env : "";
+#else
+    const std::string path;
+#endif
+    std::lock_guard<std::mutex> lk(m);
+    auto it = apis->find(path);
+    if (it != apis->end()) return *it->second;
+    RcclApi* ap = new RcclApi();
+    (*apis)[path] = ap;
+    RcclApi& a = *ap;
+    void* h = nullptr;
+    if (!path.empty()) {
+        h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    } else {
+        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-        if (!h) {
-            const char* e = dlerror();
-            a.err = std::string("cannot load librccl: ") + (e ? e : "?");
-            return;
+    }
+    if (!h) {
+        const char* e = dlerror();
+        a.err = "cannot load " + (path.empty() ? std::string("librccl") : path) + ": " + (e ? e : "?");
+        return a;
+    }
+    bool all = true;
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        if (!fn) {
+            all = false;
+            a.err = std::string("librccl lacks ") + name;
         }
-        bool all = true;
-        auto sym = [&](auto& fn, const char* name) {
-            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
-            if (!fn) {
-                all = false;
-                a.err = std::string("librccl lacks ") + name;
-            }
-        };
-        sym(a.get_unique_id, "ncclGetUniqueId");
-        sym(a.comm_init_rank, "ncclCommInitRank");
-        sym(a.comm_init_all, "ncclCommInitAll");
-        sym(a.comm_destroy, "ncclCommDestroy");
-        sym(a.send, "ncclSend");
-        sym(a.recv, "ncclRecv");
-        sym(a.group_start, "ncclGroupStart");
-        sym(a.group_end, "ncclGroupEnd");
-        sym(a.error_string, "ncclGetErrorString");
-        a.ok = all;
-    });
+    };
+    sym(a.get_unique_id, "ncclGetUniqueId");
+    sym(a.comm_init_rank, "ncclCommInitRank");
+    sym(a.comm_init_all, "ncclCommInitAll");
+    sym(a.comm_destroy, "ncclCommDestroy");
+    sym(a.send, "ncclSend");
+    sym(a.recv, "ncclRecv");
+    sym(a.group_start, "ncclGroupStart");
+    sym(a.group_end, "ncclGroupEnd");
+    sym(a.error_string, "ncclGetErrorString");
+    a.ok = all;
     return a;
 }
 }  // namespace
 
 struct rt_comm {
+    RcclApi* api = nullptr;  // the library the communicator was made with
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0, device = -1;
     // held from ncclGroupStart to ncclGroupEnd: two scenes gathering through
@@ -123,14 +145,6 @@ struct DeviceWorld {
     size_t srgb_bytes = 0;
     void* stack_ovf = nullptr;  // mesh / full tiers: traversal-stack entries beyond the LDS part
     size_t stack_ovf_bytes = 0;
-    // the full tier's wavefront variant (RT_WAVEFRONT=1; rtk_launch_frame_wf):
-    // path slots in HBM and the walk kernel's grid
-    double* wf_d = nullptr;
-    uint32_t* wf_u = nullptr;
-    uint32_t* wf_ctr = nullptr;
-    size_t wf_slots = 0;
-    int wf_grid = 0;
-    bool wf_ok = false;
     hipStream_t own_stream = nullptr;  // for parts that do not run on the caller's stream
     hipEvent_t ev_start = nullptr, ev_stop = nullptr;
     hipEvent_t ev_done = nullptr;  // after the slot's last device work (orders the next render)
@@ -181,9 +195,6 @@ static void destroy_device_world(DeviceWorld* d) {
     if (d->out) (void)hipFree(d->out);
     if (d->stack_ovf) (void)hipFree(d->stack_ovf);
     if (d->srgb) (void)hipFree(d->srgb);
-    if (d->wf_d) (void)hipFree(d->wf_d);
-    if (d->wf_u) (void)hipFree(d->wf_u);
-    if (d->wf_ctr) (void)hipFree(d->wf_ctr);
     if (d->ev_start) (void)hipEventDestroy(d->ev_start);
     if (d->ev_stop) (void)hipEventDestroy(d->ev_stop);
     if (d->ev_done) (void)hipEventDestroy(d->ev_done);
@@ -219,28 +230,31 @@ static void free_root_buffers(RenderState* r) {
 // groups could hang or swap two scenes' rows.
 struct CommSet {
     std::mutex group;
+    RcclApi* api = nullptr;
     std::vector<ncclComm_t> comms;
 };
 struct CommCache {
     std::mutex m;  // the map only
-    std::map<std::vector<int>, std::shared_ptr<CommSet>> sets;
+    std::map<std::pair<RcclApi*, std::vector<int>>, std::shared_ptr<CommSet>> sets;
 };
 static CommCache& comm_cache() {
     static CommCache* c = new CommCache();  // never destroyed: RCCL may already be torn down at exit
     return *c;
 }
-static int32_t nccl_fail(ncclResult_t e, const char* what);
-static int32_t acquire_comms(RenderState* r, const std::vector<int>& devs) {
-    if (r->comm_devices == devs && r->comm_set) return RT_OK;
+static int32_t nccl_fail(const RcclApi& nc, ncclResult_t e, const char* what);
+static int32_t acquire_comms(RenderState* r, RcclApi& nc, const std::vector<int>& devs) {
+    if (r->comm_devices == devs && r->comm_set && r->comm_set->api == &nc) return RT_OK;
     CommCache& cc = comm_cache();
     std::lock_guard<std::mutex> lk(cc.m);
-    auto it = cc.sets.find(devs);
+    const auto key = std::make_pair(&nc, devs);
+    auto it = cc.sets.find(key);
     if (it == cc.sets.end()) {
         auto set = std::make_shared<CommSet>();
+        set->api = &nc;
         set->comms.assign(devs.size(), nullptr);
-        const ncclResult_t ne = rccl().comm_init_all(set->comms.data(), (int)devs.size(), devs.data());
-        if (ne != ncclSuccess) return nccl_fail(ne, "ncclCommInitAll");
-        it = cc.sets.emplace(devs, std::move(set)).first;
+        const ncclResult_t ne = nc.comm_init_all(set->comms.data(), (int)devs.size(), devs.data());
+        if (ne != ncclSuccess) return nccl_fail(nc, ne, "ncclCommInitAll");
+        it = cc.sets.emplace(key, std::move(set)).first;
     }
     r->comm_set = it->second;
     r->comm_devices = devs;
@@ -312,7 +326,6 @@ struct FlatWorld {
     double ms = 0;
     int tier = 1;
     uint32_t stack_need = 0;
-    bool wf_ok = false;  // the full tier's wavefront variant may run this world (media fit its queue, one-pass)
     std::vector<char> blob;
     rtk::SceneView rel{};  // SceneView with byte offsets into blob instead of pointers
     size_t n_prims = 0;
@@ -404,11 +417,6 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.n_ref[rtk::K_POPXF] = 1;  // the marker's index is 0
     fw.tier = tier;
     fw.stack_need = hw.stack_need;
-    // the wavefront walk only queues media (no medium code in it): every
-    // medium must fit the queue (a walk meets each at most once) and have a
-    // one-pass boundary (rt_wf_shade tests them with boundary_onepass)
-    fw.wf_ok = tier == rtk::TIER_FULL && hw.media.size() <= RT_MEDIA_CAP;
-    for (const rtk::DMedium& m : hw.media) fw.wf_ok = fw.wf_ok && (m.planar_n || m.bsphere);
     fw.n_prims = hw.n_prims;
     fw.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return RT_OK;
@@ -450,11 +458,6 @@ static int32_t slot_for(RenderState* r, size_t k, int device, DeviceWorld*& out)
         if (bpc < 1) bpc = 1;
         d->grid[t] = bpc * prop.multiProcessorCount;
     }
-    {
-        int bpc = 0;
-        if ((e = (hipError_t)rtk_wf_walk_occupancy(&bpc)) != hipSuccess) return hip_fail(e, "occupancy query");
-        d->wf_grid = (bpc < 1 ? 1 : bpc) * prop.multiProcessorCount;
-    }
     d->cus = prop.multiProcessorCount;
     out = d;
     return RT_OK;
@@ -474,8 +477,7 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
     hipError_t e;
     const uint32_t lds_entries = rtk::lds_stack_entries(fw.tier);
     if (fw.stack_need > lds_entries) {
-        // (the full tier's wavefront walk may run more blocks than its megakernel)
-        const int blocks = fw.tier == rtk::TIER_FULL ? std::max(d->grid[fw.tier], d->wf_grid) : d->grid[fw.tier];
+        const int blocks = d->grid[fw.tier];
         const size_t need = (size_t)(fw.stack_need - lds_entries) * blocks * RT_BLOCK * sizeof(uint64_t);
         if (need > d->stack_ovf_bytes) {
             if (d->stack_ovf) (void)hipFree(d->stack_ovf);
@@ -502,7 +504,6 @@ static int32_t upload_world(rt_scene* s, DeviceWorld* d, int32_t world, int32_t 
         fix(v.texels), fix(v.perlin);
     d->view = v;
     d->tier = fw.tier;
-    d->wf_ok = fw.wf_ok;
     d->reference_bvh = reference_bvh;
     d->blob_bytes = fw.blob.size();
     d->world = world;
@@ -696,26 +697,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     float* out = p.out ? p.out : d->out;
     p.out_used = out;
     const bool run = f.rows > 0 && f.max_depth > 0;
-    // RT_WAVEFRONT=1: the full tier's frame as wavefront bounces over
-    // RT_WF_SLOTS path slots (rt_kernel.hip rt_wf_walk / rt_wf_shade; A/B)
-    const bool wavefront = d->tier == rtk::TIER_FULL && d->wf_ok && env_u32("RT_WAVEFRONT", 0) == 1;
-    if (run && wavefront) {
-        const size_t n = env_u32("RT_WF_SLOTS", 1u << 21);
-        if (n > d->wf_slots) {
-            if (d->wf_d) (void)hipFree(d->wf_d);
-            if (d->wf_u) (void)hipFree(d->wf_u);
-            d->wf_d = nullptr, d->wf_u = nullptr, d->wf_slots = 0;
-            if ((e = hipMalloc(&d->wf_d, n * 17 * sizeof(double))) != hipSuccess) return fail(hip_fail(e, "hipMalloc wavefront slots"));
-            if ((e = hipMalloc(&d->wf_u, n * 19 * sizeof(uint32_t))) != hipSuccess)
-                return fail(hip_fail(e, "hipMalloc wavefront slots"));
-            d->wf_slots = n;
-        }
-        if (!d->wf_ctr && (e = hipMalloc(&d->wf_ctr, 256)) != hipSuccess) return fail(hip_fail(e, "hipMalloc wavefront counters"));
-        e = rtk_launch_frame_wf(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, p.stream, d->tier,
-                                d->wf_grid, d->params, d->stack_ovf, d->wf_d, d->wf_u, d->wf_ctr, (uint32_t)n,
-                                env_u32("RT_WF_CHECK", 32));
-        if (e != hipSuccess) return fail(hip_fail(e, "wavefront launch"));
-    } else if (run) {
+    if (run) {
         e = rtk_launch_frame(&d->view, &f, d->queue, d->partial, d->stats, out, srgb, cam->toon_map, p.stream, d->tier,
                              d->grid[d->tier], d->params, d->stack_ovf);
         if (e != hipSuccess) return fail(hip_fail(e, "kernel launch"));
@@ -740,8 +722,8 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     d->last_stream = p.stream;
 }
 
-static int32_t nccl_fail(ncclResult_t e, const char* what) {
-    return set_error(RT_EDEVICE, std::string(what) + ": " + rccl().error_string(e));
+static int32_t nccl_fail(const RcclApi& nc, ncclResult_t e, const char* what) {
+    return set_error(RT_EDEVICE, std::string(what) + ": " + nc.error_string(e));
 }
 
 // Root-side buffers of a gather on the current (root) device.
@@ -888,7 +870,8 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         const uint32_t W = f_all.W, rows = f_all.rows;
         const size_t slice = (size_t)part_rows(rows, 0, n_parts) * W * 3;  // part 0 has the most rows
         const size_t row_floats = (size_t)W * 3;
-        RcclApi& nc = rccl();
+        // a communicator's own library; a device list's, the current one
+        RcclApi& nc = comm ? *comm->api : rccl();
         if ((e = hipSetDevice(root.device)) != hipSuccess) return abort_render(hip_fail(e, "hipSetDevice"));
         hipStream_t rs = root.stream;
         if (is_root) {
@@ -900,6 +883,14 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         bool distinct = true;
         for (uint32_t i = 0; i < nd && !comm; ++i)
             for (uint32_t j = i + 1; j < nd; ++j) distinct = distinct && opts->devices[i] != opts->devices[j];
+#ifdef RT_CHECK
+        // check build only: RT_CHECK_RCCL_DUPS=1 sends a device list with a
+        // repeated device through the RCCL group too (real RCCL refuses two
+        // ranks on one device; the test stand-in of RT_RCCL_LIB accepts them),
+        // so the one-GPU box runs the distinct-device gather's sends,
+        // receives and slice offsets (tests/test_gather_standin_gpu.py)
+        if (!comm && std::getenv("RT_CHECK_RCCL_DUPS") && std::getenv("RT_CHECK_RCCL_DUPS")[0] == '1') distinct = true;
+#endif
         if (comm) {
             if (!nc.ok) return abort_render(set_error(RT_EDEVICE, nc.err));
             std::lock_guard<std::mutex> glk(comm->group);  // the whole group, enqueued at once
@@ -916,11 +907,11 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                         ne = nc.recv(r->staging_srgb + q * slice, n_q, ncclUint8, (int)q, comm->comm, rs);
                 }
             const ncclResult_t ge = nc.group_end();
-            if (ne != ncclSuccess) return abort_render(nccl_fail(ne, "ncclSend/ncclRecv"));
-            if (ge != ncclSuccess) return abort_render(nccl_fail(ge, "ncclGroupEnd"));
+            if (ne != ncclSuccess) return abort_render(nccl_fail(nc, ne, "ncclSend/ncclRecv"));
+            if (ge != ncclSuccess) return abort_render(nccl_fail(nc, ge, "ncclGroupEnd"));
         } else if (distinct && nc.ok) {
             const std::vector<int> devs(opts->devices, opts->devices + nd);
-            if ((rc = acquire_comms(r, devs)) != RT_OK) return abort_render(rc);
+            if ((rc = acquire_comms(r, nc, devs)) != RT_OK) return abort_render(rc);
             CommSet& cs = *r->comm_set;
             std::lock_guard<std::mutex> glk(cs.group);  // the whole group, enqueued at once
             ncclResult_t ne = nc.group_start();
@@ -939,8 +930,8 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
                                  cs.comms[0], rs);
             }
             const ncclResult_t ge = nc.group_end();
-            if (ne != ncclSuccess) return abort_render(nccl_fail(ne, "ncclSend/ncclRecv"));
-            if (ge != ncclSuccess) return abort_render(nccl_fail(ge, "ncclGroupEnd"));
+            if (ne != ncclSuccess) return abort_render(nccl_fail(nc, ne, "ncclSend/ncclRecv"));
+            if (ge != ncclSuccess) return abort_render(nccl_fail(nc, ge, "ncclGroupEnd"));
         } else {
             // a device listed twice (one communicator per device is all RCCL
             // allows) or no librccl: peer copies onto the root
@@ -1201,7 +1192,7 @@ int32_t rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]) {
     if (!nc.ok) return set_error(RT_EDEVICE, nc.err);
     ncclUniqueId u;
     ncclResult_t e = nc.get_unique_id(&u);
-    if (e != ncclSuccess) return nccl_fail(e, "ncclGetUniqueId");
+    if (e != ncclSuccess) return nccl_fail(nc, e, "ncclGetUniqueId");
     static_assert(sizeof(u) == RT_COMM_ID_BYTES, "ncclUniqueId size");
     std::memcpy(id, &u, sizeof u);
     return RT_OK;
@@ -1226,9 +1217,10 @@ rt_comm* rt_comm_init(const uint8_t id[RT_COMM_ID_BYTES], int32_t nranks, int32_
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     rt_comm* c = new rt_comm();
+    c->api = &nc;
     ncclResult_t e = nc.comm_init_rank(&c->comm, nranks, u, rank);
     if (e != ncclSuccess) {
-        nccl_fail(e, "ncclCommInitRank");
+        nccl_fail(nc, e, "ncclCommInitRank");
         delete c;
         return nullptr;
     }
@@ -1240,7 +1232,7 @@ rt_comm* rt_comm_init(const uint8_t id[RT_COMM_ID_BYTES], int32_t nranks, int32_
 
 void rt_comm_destroy(rt_comm* c) {
     if (!c) return;
-    if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
+    if (c->comm && c->api && c->api->ok) (void)c->api->comm_destroy(c->comm);
     delete c;
 }
 

@@ -5,7 +5,7 @@ variant renders the same frame; path-kernel time from the library's HIP
 events.  Usage: python scripts/ab.py [spp] [reps] [variant ...]; a variant is a library
 name (librt_ab_<name>.so) optionally followed by @VAR=val,... (environment
 variables set while its world is flattened and its frames render, e.g.
-base@RT_WAVEFRONT=1).
+base@RT_PART_SAMPLES=2).
 AB_WORKLOAD=c3|c4|c5 renders that config's scene (C5 at 1920 wide) instead of C2."""
 import ctypes
 import glob
@@ -67,7 +67,7 @@ for _ in range(reps):
         scene, world, lights, cam, ref = runs[n]
         env = dict(kv.split("=", 1) for kv in n.partition("@")[2].split(",") if kv)
         saved = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)  # (knobs read per render, e.g. RT_WAVEFRONT)
+        os.environ.update(env)  # (knobs read per render, e.g. RT_PART_SAMPLES)
         lin, _, st = cam.render(world, lights, seed=1, want_srgb=False)
         for k, v in saved.items():
             if v is None:

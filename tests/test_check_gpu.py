@@ -24,37 +24,53 @@ CHECK_SO = os.path.join(ROOT, "raytracer-2025_amd", "librt_mi355x_check.so")
 
 @pytest.fixture(scope="module")
 def check_api(capi, gpu):
-    if not os.path.exists(CHECK_SO):
-        pytest.skip("check build absent: make -C raytracer-2025_amd check")
-    return capi.Api(ctypes.CDLL(CHECK_SO), "rt_")
+    # a build product (__graft_entry__.build() makes it): absent is a failure
+    assert os.path.exists(CHECK_SO), "check build absent: make -C raytracer-2025_amd check (__graft_entry__.build())"
+    api = capi.Api(ctypes.CDLL(CHECK_SO), "rt_")
+    assert not api.missing, api.missing
+    return api
 
 
-def _worlds(rt, scenes, api):
+@pytest.fixture(scope="module")
+def terrain(scenes, tmp_path_factory):
+    return scenes.write_terrain_obj(str(tmp_path_factory.mktemp("check_terrain")), 24)
+
+
+def _worlds(rt, scenes, api, terrain):
     s = rt.Scene(api)
     yield "spheres", s, *scenes.random_spheres(s, 48, 4)
     s = rt.Scene(api)
     yield "cornell", s, *scenes.cornell_smoke(s, 40, 4)
     s = rt.Scene(api)
     yield "final", s, *scenes.final_scene(s, 48, 4, 8, aspect_ratio=16 / 9)
+    s = rt.Scene(api)
+    yield "terrain", s, *scenes.obj_terrain(s, terrain, 64, 4)
 
 
-def test_check_build_renders_like_the_product(check_api, gpu, rt, scenes):
-    """No ref past its array on the basic, flat and full tiers, and the same
-    bits as the product library."""
-    for (name, s, world, lights, cam), (_, s2, world2, lights2, cam2) in zip(_worlds(rt, scenes, check_api),
-                                                                            _worlds(rt, scenes, gpu)):
+def test_check_build_renders_like_the_product(check_api, gpu, rt, scenes, capi, terrain):
+    """No ref past its array on the basic, mesh (OBJ terrain), flat and full
+    tiers, and the same bits as the product library."""
+    tiers = set()
+    for (name, s, world, lights, cam), (_, s2, world2, lights2, cam2) in zip(_worlds(rt, scenes, check_api, terrain),
+                                                                            _worlds(rt, scenes, gpu, terrain)):
         lin, _, st = cam.render(world, lights, seed=3, want_srgb=False)
-        ref, _, _ = cam2.render(world2, lights2, seed=3, want_srgb=False)
+        ref, _, st2 = cam2.render(world2, lights2, seed=3, want_srgb=False)
         np.testing.assert_array_equal(lin, ref, err_msg=name)
+        info = capi.RtWorldInfo()
+        bg = cam.background.h if cam.background is not None else -1
+        check_api.check(check_api.world_info_get(s.s, world.h, -1 if lights is None else lights.h, bg, 0,
+                                                 ctypes.byref(info)))
+        tiers.add(info.kernel_tier)
+    assert tiers == {0, 1, 2, 3}, tiers
 
 
-@pytest.mark.parametrize("workload", ["spheres", "final"])
-def test_check_build_reports_a_bad_ref(check_api, rt, scenes, capi, workload, monkeypatch):
+@pytest.mark.parametrize("workload", ["spheres", "final", "terrain"])
+def test_check_build_reports_a_bad_ref(check_api, rt, scenes, capi, workload, monkeypatch, terrain):
     """RT_CHECK_INJECT=1: the flattened world's first primitive slot names one
     record past its array (basic tier: a sphere; full tier: a sphere or quad);
     the render must fail with RT_EPANIC and say which ref."""
     monkeypatch.setenv("RT_CHECK_INJECT", "1")
-    for name, s, world, lights, cam in _worlds(rt, scenes, check_api):
+    for name, s, world, lights, cam in _worlds(rt, scenes, check_api, terrain):
         if name != workload:
             continue
         with pytest.raises(capi.RtError) as e:

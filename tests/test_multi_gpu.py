@@ -175,19 +175,3 @@ def test_two_threads_share_a_communicator(gpu, rt, scenes):
     finally:
         gpu.comm_destroy(comm)
 
-
-def test_wavefront_full_tier_is_bit_equal(gpu, rt, scenes, monkeypatch):
-    """RT_WAVEFRONT=1: the full tier's frame as wavefront bounces (rt_wf_walk /
-    rt_wf_shade over path slots in HBM, rt_kernel.hip) equals the megakernel's
-    frame bit for bit: the same queue entries, samples in s_j order and RNG
-    keys; the media a walk queues tested in the shade kernel.  Few slots
-    (RT_WF_SLOTS) so that slots take several entries each."""
-    s = rt.Scene(gpu)
-    world, lights, cam = scenes.final_scene(s, 96, 16, 10, aspect_ratio=16 / 9)
-    ref, _, st0 = cam.render(world, lights, seed=9, want_srgb=False)
-    monkeypatch.setenv("RT_WAVEFRONT", "1")
-    monkeypatch.setenv("RT_WF_SLOTS", "4096")
-    monkeypatch.setenv("RT_WF_CHECK", "4")
-    lin, _, st = cam.render(world, lights, seed=9, want_srgb=False)
-    np.testing.assert_array_equal(lin, ref)
-    assert st.rays == st0.rays and st.samples == st0.samples and st.panics == 0
