@@ -1846,6 +1846,13 @@ struct Draws {
 #ifndef RT_UNIFIED_DRAWS
 #define RT_UNIFIED_DRAWS 1
 #endif
+// basic tier: in-walk restarts of missed / pathless lanes (0 = off; A/B)
+#ifndef RT_WALK_RESTART
+#define RT_WALK_RESTART 0
+#endif
+#ifndef RT_WALK_RESTART_MIN
+#define RT_WALK_RESTART_MIN 16
+#endif
 
 // ---- general materials (tier FULL_GL): DiffuseLight / Mix wrappers nested
 // up to RT_MAT_DEPTH levels (rt_scene.cpp checks), Mix::from_image ratios.
@@ -2395,6 +2402,28 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         // panic, no scatter) starts its next sample one iteration later.
         bool no_path = true;  // the lane starts a sample at its next post-walk stage
         constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC : RT_SHADE_BATCH_MESH;
+        // ---- Camera::get_ray (camera.rs:247-273), vertex 0, from the iteration's draws
+        auto camera_ray = [&](const Draws& Dr) {
+            const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
+            double xi0 = Dr.xi0, xi1 = Dr.xi1;
+            D3 origin = F.center;
+            if (F.defocus) {  // vec3.rs:63-69: theta = 2 pi Dr.xi0, r = sqrt(Dr.xi1)
+                rng.pair(0u, 0u, xi0, xi1);
+                const double rr = sqrt(Dr.xi1);
+                origin = (F.center + ((rr * Dr.cs) * F.disk_u)) + ((rr * Dr.sn) * F.disk_v);
+            }
+            const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
+            const double oy = (((double)s_j + xi1) * F.recip_sqrt_spp) - 0.5;
+            const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
+            ray.o = origin;
+            ray.d = ps - origin;
+            ray.time = 0.0;  // read only by moving spheres (full tiers): its draw is skipped
+            beta = d3(1, 1, 1);
+            L = d3(0, 0, 0);
+            vertex = 1;
+            no_path = false;
+        };
+        bool quit = false;  // RT_WALK_RESTART: the queue ran out for this lane inside a walk phase
         for (;;) {
             RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
 #ifdef RT_WAVE_TRACE
@@ -2419,7 +2448,44 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                     return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
                 }
             };
-            if constexpr (BATCH >= 64) {
+            if constexpr (BATCH >= 64 && TIER == TIER_BASIC && RT_WALK_RESTART > 0) {
+                // In-walk restarts (A/B): while the wave walks, lanes whose walk
+                // missed (the sample ends at the sky) or that hold no path start
+                // their next sample's camera ray at once, in rounds of at least
+                // RT_WALK_RESTART such lanes while at least RT_WALK_RESTART_MIN
+                // lanes still walk -- the walk phase's idle lanes take new walks
+                // instead of waiting for the wave's longest walk.  Same draws,
+                // same sums in s_j order: the same bits.
+                for (;;) {
+                    if (walking) walking = step();
+                    const unsigned long long wk = __ballot(walking);
+                    if (wk == 0) break;
+                    const bool restart = !walking && !quit && (no_path || !T.found);
+                    const unsigned long long rm = __ballot(restart);
+                    if ((uint32_t)__popcll(rm) < RT_WALK_RESTART || (uint32_t)__popcll(wk) < RT_WALK_RESTART_MIN)
+                        continue;
+                    if (restart && !no_path) {  // the miss: Environment::value, and the sample ends
+                        bool panic = false;
+                        shade<TIER>(S, ray, beta, L, rng, false, T.hit, panic);
+                        if (panic) ++n_panics;
+                        finish_sample();
+                        no_path = true;
+                    }
+                    if (!quit && !refill()) quit = true;  // the wave's pool: uniform control flow
+                    if (restart && !quit) {
+                        rng.sample = (sie & 0xFFFFu) * F.S + s_j;
+                        Draws Dr;
+                        rng.pair(0u, F.defocus ? 1u : 0u, Dr.xi0, Dr.xi1);
+                        k_sincos_2pi(Dr.xi0, &Dr.sn, &Dr.cs);
+                        camera_ray(Dr);
+                        rng.begin(vertex);
+                        ++n_rays;
+                        trace_begin<TIER>(S, ray, T);
+                        walking = true;
+                    }
+                }
+                if (quit) break;
+            } else if constexpr (BATCH >= 64) {
 #ifdef RT_WAVE_TRACE
                 while (walking) walking = step(), ++trace_steps;
 #else
@@ -2485,25 +2551,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 }
                 RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_d;)
             } else {
-                // ---- Camera::get_ray (camera.rs:247-273), vertex 0
-                const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
-                double xi0 = Dr.xi0, xi1 = Dr.xi1;
-                D3 origin = F.center;
-                if (F.defocus) {  // vec3.rs:63-69: theta = 2 pi Dr.xi0, r = sqrt(Dr.xi1)
-                    rng.pair(0u, 0u, xi0, xi1);
-                    const double rr = sqrt(Dr.xi1);
-                    origin = (F.center + ((rr * Dr.cs) * F.disk_u)) + ((rr * Dr.sn) * F.disk_v);
-                }
-                const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
-                const double oy = (((double)s_j + xi1) * F.recip_sqrt_spp) - 0.5;
-                const D3 ps = (F.pixel00 + (((double)px + ox) * F.du)) + (((double)py + oy) * F.dv);
-                ray.o = origin;
-                ray.d = ps - origin;
-                ray.time = 0.0;  // read only by moving spheres (full tiers): its draw is skipped
-                beta = d3(1, 1, 1);
-                L = d3(0, 0, 0);
-                vertex = 1;
-                no_path = false;
+                camera_ray(Dr);
                 RT_DIAG_ONLY(dg.cyc_refill += __builtin_amdgcn_s_memtime() - t_d;)
             }
         }
