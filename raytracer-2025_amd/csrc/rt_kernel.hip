@@ -61,10 +61,14 @@ struct Diag {
     // active lanes all read one record (of them node records), active lanes,
     // lanes reading the first active lane's record
     unsigned long long u_steps = 0, u_uniform = 0, u_uniform_node = 0, u_active = 0, u_same = 0;
+    // ... steps whose active lanes all read nodes of the top 5 / 21 / 85 / 341
+    // (rth::bvh4_convert numbers the top levels first, breadth-first), and
+    // node reads of lanes at those nodes (lane counts)
+    unsigned long long u_top[4] = {0, 0, 0, 0}, l_top[4] = {0, 0, 0, 0}, l_node = 0;
 #endif
 };
 #ifdef RT_DIAG
-constexpr int RT_DIAG_N = 24;
+constexpr int RT_DIAG_N = 33;
 __device__ unsigned long long g_diag[RT_DIAG_N];
 #define RT_DIAG_ONLY(x) x
 #else
@@ -1156,6 +1160,14 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                     ++dg.u_uniform;
                     if (kind == K_BVH) ++dg.u_uniform_node;
                 }
+            }
+            constexpr uint32_t TOPK[4] = {5u, 21u, 85u, 341u};
+            if (kind == K_BVH) ++dg.l_node;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const bool top = kind == K_BVH && idx < TOPK[k];
+                if (top) ++dg.l_top[k];
+                if (__ballot(top) == act && __lane_id() == (uint32_t)(__ffsll((long long)act) - 1)) ++dg.u_top[k];
             }
         }
 #endif
@@ -2825,6 +2837,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     atomicAdd(&g_diag[18], dg.u_uniform_node);
     atomicAdd(&g_diag[19], dg.u_active);
     atomicAdd(&g_diag[20], dg.u_same);
+    for (int k = 0; k < 4; ++k) {
+        atomicAdd(&g_diag[24 + k], dg.u_top[k]);
+        atomicAdd(&g_diag[28 + k], dg.l_top[k]);
+    }
+    atomicAdd(&g_diag[32], dg.l_node);
 #endif
 #ifdef RT_WAVE_TRACE
     hist.flush();

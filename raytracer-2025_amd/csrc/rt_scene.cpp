@@ -1524,6 +1524,7 @@ namespace rth {
 #endif
 
 namespace rth {
+constexpr uint32_t BVH4_TOP = 341;  // 1 + 4 + 16 + 64 + 256
 // Collapses the two-box BVHs of a world into 4-wide nodes: starting from a
 // node's two children, the inner child with the largest box (surface area) is
 // replaced by its own children until there are four or no inner child is left
@@ -1667,6 +1668,45 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
     const uint32_t sn = 1 + need(root);
     if (sn > max_need) return sn;
     if (out.size() > max_nodes) return UINT32_MAX;
+    if (!filter_spheres) {
+        // the mesh / full tiers: the first BVH4_TOP nodes breadth-first from the
+        // world's root BVH (levels 0-4 of a full 4-wide tree) take indices
+        // 0 .. BVH4_TOP - 1, the rest keep the build's depth-first order after
+        // them -- so that "index < K" names the top levels (the diagnostic
+        // build's top-level step counts).  A layout only: the walk
+        // visits the same nodes in the same order.
+        std::vector<uint32_t> seeds;
+        if (rtk::ref_kind(root) == rtk::K_BVH) seeds.push_back(rtk::ref_index(root));
+        if (rtk::ref_kind(root) == rtk::K_LIST)
+            for (uint32_t p = rtk::ref_index(root); lists[p] != REF_NONE; ++p)
+                if (rtk::ref_kind(lists[p]) == rtk::K_BVH) seeds.push_back(rtk::ref_index(lists[p]));
+        constexpr uint32_t UNPLACED = UINT32_MAX;  // (REF_NONE is 0: a valid index)
+        std::vector<uint32_t> order, newidx(out.size(), UNPLACED);
+        order.reserve(out.size());
+        for (size_t head = 0; head < seeds.size() && order.size() < BVH4_TOP; ++head) {
+            const uint32_t n = seeds[head];
+            if (newidx[n] != UNPLACED) continue;
+            newidx[n] = (uint32_t)order.size();
+            order.push_back(n);
+            for (int i = 0; i < 4; ++i)
+                if (rtk::ref_kind(out[n].ref[i]) == rtk::K_BVH) seeds.push_back(rtk::ref_index(out[n].ref[i]));
+        }
+        for (uint32_t n = 0; n < (uint32_t)out.size(); ++n)
+            if (newidx[n] == UNPLACED) newidx[n] = (uint32_t)order.size(), order.push_back(n);
+        auto remap = [&](uint32_t& r) {
+            if (rtk::ref_kind(r) == rtk::K_BVH) r = rtk::make_ref(rtk::K_BVH, newidx[rtk::ref_index(r)]);
+        };
+        std::vector<rtk::DNode4> perm(out.size());
+        for (uint32_t k = 0; k < (uint32_t)order.size(); ++k) {
+            perm[k] = out[order[k]];
+            for (int i = 0; i < 4; ++i) remap(perm[k].ref[i]);
+        }
+        out.swap(perm);
+        for (uint32_t& r : lists) remap(r);
+        for (rtk::DXform& x : xforms) remap(x.child);
+        for (rtk::DMedium& m : media) remap(m.boundary);
+        remap(root);
+    }
     hw.nodes4 = std::move(out);
     hw.nodes.clear();  // the two-box nodes are not walked any more
     hw.list_children = std::move(lists);

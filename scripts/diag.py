@@ -37,7 +37,7 @@ elif wl == "c5":
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
-buf = (ctypes.c_ulonglong * 24)()
+buf = (ctypes.c_ulonglong * 33)()
 lib.rt_diag_counters(buf, 1)
 _, _, st = cam.render(world, lights, seed=1, want_srgb=False)
 lib.rt_diag_counters(buf, 0)
@@ -72,6 +72,12 @@ out = {
     # iteration's Philox block and sincos (the rest of refill+camera: the
     # walk set-up and the camera rays)
     "after_walk_share": {"miss+finish": c[21] / tot, "queue_refill": c[22] / tot, "draws": c[23] / tot},
-    "raw": c[:24],
+    # mesh / full tiers: wave steps whose active lanes all read nodes among the
+    # top 5 / 21 / 85 / 341 (levels 0-1 / 0-2 / 0-3 / 0-4 of a full 4-wide
+    # tree: rth::bvh4_convert numbers them first), and the share of all node
+    # reads that are of those nodes (lane count)
+    "top_uniform_step_share": {str(k): (c[24 + i] / c[16] if c[16] else None) for i, k in enumerate((5, 21, 85, 341))},
+    "top_node_read_share": {str(k): (c[28 + i] / c[32] if c[32] else None) for i, k in enumerate((5, 21, 85, 341))},
+    "raw": c[:33],
 }
 print(json.dumps(out, indent=1))
