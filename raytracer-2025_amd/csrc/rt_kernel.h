@@ -9,7 +9,7 @@
 #define RT_BLOCK 256        // 4 waves of 64 (mesh and full tiers)
 // Basic tier: one 1024-thread block per CU (16 waves, 4 per SIMD: the same
 // 128-VGPR budget) so that one LDS copy of the world's 4-wide nodes serves
-// the whole CU.  LDS: stack entries * 1024 * 4 B (RT_STACK4B) + the sphere
+// the whole CU.  LDS: stack entries * 1024 * 4 B + the sphere
 // queue (RT_PEND_CAP * 1024 * 2 B) + RT_NODE_LDS_BYTES of nodes <= 160 KiB.
 #ifndef RT_BLOCK_BASIC
 #define RT_BLOCK_BASIC 1024
@@ -25,32 +25,18 @@
 // (sphere-count scaling)
 #define RT_NODE_LDS_BYTES 73696
 #endif
-#ifndef RT_MESH_PARK
-// mesh tier: the walk state of lanes whose walk carries over a shading batch
-// is parked in LDS (8 words: 8 KiB per block) across the shading round
-#define RT_MESH_PARK 1
-#endif
 #ifndef RT_STACK_MESH
-// mesh tier: 20 entries = 40 KiB in LDS (4 blocks: the whole 160 KiB), deeper
-// entries in a global overflow column (C4: -1.6 % against 16); 16 (32 KiB)
-// with the 8-KiB park area
-#if RT_MESH_PARK
+// mesh tier: 16 entries = 32 KiB in LDS beside the 8-KiB park area (the walk
+// state of lanes whose walk carries over a shading batch: 8 words), 40 KiB
+// per block, 4 blocks: the whole 160 KiB; deeper entries in a global
+// overflow column
 #define RT_STACK_MESH 16
-#else
-#define RT_STACK_MESH 20
-#endif
 #endif
 #ifndef RT_STACK_FULL
 #define RT_STACK_FULL 16    // full tiers, likewise
 #endif
 #ifndef RT_STACK_FLAT
 #define RT_STACK_FLAT 4     // full-flat tier (lists only: C3 needs 4); deeper ones overflow
-#endif
-#ifndef RT_FLAT_PARK_RAY
-#define RT_FLAT_PARK_RAY 1  // full-flat tier: the world ray too (read back where the walk needs it)
-#endif
-#ifndef RT_FLAT_LDS_STATE
-#define RT_FLAT_LDS_STATE 1 // full-flat tier: beta, L, acc and the item fields live in LDS across the walk
 #endif
 #define RT_STACK_MAX 96     // LDS + overflow entries (mesh and full tiers)
 #ifndef RT_MEDIA_CAP

@@ -363,9 +363,6 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
     return true;
 }
 
-#ifndef RT_UV_ON_DEMAND
-#define RT_UV_ON_DEMAND 1  // a planar hit's (u, v) only when its material or remap reads them
-#endif
 // quad.rs:71-102 / triangle.rs:69-98 on the record's values: unit normal n,
 // parm_d D, anchor Q, edges u / v, w = n / |n|^2
 __device__ __forceinline__ bool planar_t_v(const D3 n, const double D, const D3 Q, const D3 u, const D3 v, const D3 w,
@@ -428,15 +425,12 @@ __device__ __forceinline__ D3 quat_rotate(double w, double x, double y, double z
               ((pw * cz + px * cy) - py * cx) + pz * w);
 }
 // Transform::detransform (shapes.rs:80-84): conj(q).rotate_vector(v - offset) / scale
-#ifndef RT_XF_UNIT
 // 1: a Transform whose scale is exactly (1, 1, 1) (the reference's `None`,
 // every Transform of C3 and C5) skips the three f64 divisions: x / 1.0 is x,
 // bit for bit, NaN, infinities and signed zeros included
-#define RT_XF_UNIT 1
-#endif
 __device__ __forceinline__ D3 xf_in(const DXform& X, D3 v) {
     const D3 p = quat_rotate(X.q[0], -X.q[1], -X.q[2], -X.q[3], v - d3(X.off[0], X.off[1], X.off[2]));
-    if (RT_XF_UNIT && (X.flags & XF_UNIT_SCALE)) return p;
+    if (X.flags & XF_UNIT_SCALE) return p;
     return p / d3(X.scale[0], X.scale[1], X.scale[2]);
 }
 // Transform::transform (shapes.rs:74-78): q.rotate_vector(v * scale) + offset
@@ -478,9 +472,6 @@ struct HitInfo {
 // per half-wave.  With OVF, entries k >= CAP (deep triangle BVHs) live in the
 // lane's column of a global overflow buffer, [k - CAP][lane of the grid], so
 // the LDS part stays small enough for 4 blocks per CU.
-#ifndef RT_STACK4B
-#define RT_STACK4B 1
-#endif
 template <uint32_t CAP, bool OVF, uint32_t BLK>
 struct StackT {
     RT_LDS uint2* base;  // explicitly LDS: a select against ovf must not become a flat pointer
@@ -505,7 +496,7 @@ struct StackT {
         return base[sp * BLK];
     }
 };
-// Basic tier, RT_STACK4B: 4-B entries -- a list flag and a 15-bit node / list
+// Basic tier: 4-B entries -- a list flag and a 15-bit node / list
 // index, and the upper 16 bits of the entry distance (a positive f32 cut to
 // 16 bits is rounded down: the cull stays conservative; -inf stays -inf).
 // The block's stack takes half the LDS; the rest parks walk state.
@@ -551,7 +542,7 @@ __device__ __forceinline__ uint32_t pop_w(const Stack& stk, uint32_t& sp, float 
     }
     return 0u;
 }
-template <int TIER, bool B4 = TIER == TIER_BASIC && RT_STACK4B>
+template <int TIER, bool B4 = TIER == TIER_BASIC>
 struct StackSel {
     using type = StackT<lds_stack_entries(TIER), TIER != TIER_BASIC, TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK>;
 };
@@ -639,38 +630,23 @@ __device__ __forceinline__ uint32_t pop(const Stack& stk, uint32_t& sp, uint32_t
 }
 
 constexpr float NO_CULL = -__builtin_huge_valf();
-#ifndef RT_FLAT_LIST_BOXES
 // The flat tier tests the f32 box of a compound list element (a Transform, a
 // ConstantMedium, a nested list) before entering it, with the ray's f32 form
 // made on the spot: a ray that misses the box skips the element's whole
 // walk -- for C3's smoke box the two boundary walks of media_phase.  (Testing
 // every element's box, primitives included, with the f32 ray parked in LDS
 // was 4.6 % slower: a wall's box test costs what its exact test does.)
-#define RT_FLAT_LIST_BOXES 1
-#endif
 template <int TIER>
-constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT && RT_FLAT_LIST_BOXES; }
-#ifndef RT_UNIFIED_LOAD
-#define RT_UNIFIED_LOAD 1  // mesh / full tiers: one load per walk step for node / planar / sphere records
-#endif
+constexpr bool flat_boxes() { return TIER == TIER_FULL_FLAT; }
 template <int TIER>
 constexpr bool unified_load() {
-    return ((TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4)) && RT_UNIFIED_LOAD;
+    return (TIER == TIER_MESH && RT_MESH_BVH4) || (tier_full_bvh(TIER) && RT_FULL_BVH4);
 }
 // the two doubles of a float4 read from a double record
 __device__ __forceinline__ double f4_lo(float4 q) { return __hiloint2double(__float_as_int(q.y), __float_as_int(q.x)); }
 __device__ __forceinline__ double f4_hi(float4 q) { return __hiloint2double(__float_as_int(q.w), __float_as_int(q.z)); }
-#ifndef RT_FLAT_RUNS
-#define RT_FLAT_RUNS 1  // the flat tier's list step tests a whole planar run (DBoxF::run)
-#endif
 template <int TIER>
-constexpr bool flat_runs() { return TIER == TIER_FULL_FLAT && RT_FLAT_RUNS; }
-#ifndef RT_FLAT_MEDIA_IN_LIST
-#define RT_FLAT_MEDIA_IN_LIST 1  // the flat tier queues a list's media in the list step
-#endif
-#ifndef RT_FLAT_BOUNDARY_BOXES
-#define RT_FLAT_BOUNDARY_BOXES 0  // the medium boundary walks test element boxes too
-#endif
+constexpr bool flat_runs() { return TIER == TIER_FULL_FLAT; }
 
 // The flat tier's list step tests an element's f32 box (list_boxes, rounded
 // outward; the conservative slab of rt_slab.h) before the element: a ray
@@ -716,12 +692,6 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
             cur = REF_NONE;
             if (child == REF_NONE) continue;
             const uint32_t nxt = S.list_children[li + 1] != REF_NONE ? make_ref(K_LIST, li + 1) : REF_NONE;
-            if constexpr (!BVH && RT_FLAT_BOUNDARY_BOXES && RT_FLAT_LIST_BOXES) {
-                if (!list_box_hit(S, li, rf, tmin_f, cl.c_f)) {
-                    cur = nxt;
-                    continue;
-                }
-            }
             const uint32_t ck = ref_kind(child);
             if (ck == K_SPHERE || ck == K_QUAD || ck == K_TRI || ck == K_MSPHERE) {
                 cur = child;
@@ -799,9 +769,6 @@ __device__ bool boundary_t(const SceneView& S, uint32_t root, const Ray& r0, dou
 // ConstantMedium::hit (volume.rs:37-73) of medium idx for ray r in the
 // medium's frame, interval [tmin, tmax]: the two boundary hits are one
 // boundary walk run twice (one copy of the walk in the code).
-#ifndef RT_MED_ONEPASS
-#define RT_MED_ONEPASS 1
-#endif
 // The two boundary hits of a boundary made of one sphere or of planar_n
 // consecutive quads / triangles (rt_scene.cpp planar_boundary) in one pass.  A
 // planar test's t and inside decision do not depend on the interval (quad.rs:
@@ -869,7 +836,7 @@ __device__ __forceinline__ bool medium_hit(const SceneView& S, uint32_t idx, con
     const DMedium M = S.media[idx];
     const double NINF = -__builtin_huge_val(), PINF = __builtin_huge_val();
     double t1 = 0.0, t2 = 0.0, lo = NINF;
-    if (RT_MED_ONEPASS && (M.planar_n || M.bsphere)) {
+    if (M.planar_n || M.bsphere) {
         if (!boundary_onepass(S, M, r, t1, t2)) return false;
     } else {
 #pragma nounroll
@@ -941,7 +908,7 @@ __device__ __forceinline__ void trace_begin(const SceneView& S, const Ray& wr, T
     }
 }
 
-// Mesh tier with shading batches (RT_MESH_PARK): the same 8 words; the f32
+// Mesh tier with shading batches: the same 8 words; the f32
 // ray, |d|^2 and its reciprocal are made again from the world ray on resume.
 template <class Park>
 __device__ __forceinline__ void trace_park(const Trav<TIER_MESH>& T, Park pk) {
@@ -1005,7 +972,7 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_BASIC>& T,
     T.sf = make_sphf(o, d);
 }
 // The world-frame ray as the walk reads it: a register copy, or (full-flat
-// tier, RT_FLAT_PARK_RAY) the lane's LDS copy, read only where a walk step
+// tier) the lane's LDS copy, read only where a walk step
 // needs it (leaving a Transform, the media phase) so that it holds no
 // registers across the walk.
 struct RayReg {
@@ -1103,7 +1070,7 @@ __device__ __forceinline__ bool trace_step(const SceneView& S, const WR& wrr, Tr
                 // a ConstantMedium element whose box the ray meets is queued
                 // for the media phase right here (K_MEDIUM below), without a
                 // step of its own and the pop of the rest of the list
-                const bool queue = RT_FLAT_MEDIA_IN_LIST && in_box && ck == K_MEDIUM && T.nmed < RT_MEDIA_CAP;
+                const bool queue = in_box && ck == K_MEDIUM && T.nmed < RT_MEDIA_CAP;
                 if (queue) {
                     med.set(T.nmed, make_uint4(ref_idx(S, child), T.nxf, T.xfs.a, T.xfs.b));
                     ++T.nmed;
@@ -1286,7 +1253,6 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 #ifndef RT_DEFER_THRESH
 #define RT_DEFER_THRESH 48  // lanes with a queued sphere that trigger a sphere round
 #endif
-#ifndef RT_DEFER_REL
 // ... or 3/4 of the lanes still in the walk, when fewer than 64 are; and any
 // one of them when at most RT_DEFER_THIN are: a wave thinned out at the end
 // of a launch tests its queued spheres at once instead of walking on with an
@@ -1295,8 +1261,6 @@ __device__ __forceinline__ void media_phase(const SceneView& S, const WR& wrr, T
 // nothing).  Measured within noise on the whole frame and on the 1/8 shard:
 // the slow last waves of the lane trace were the exit atomics' (the kernel's
 // end), not this.
-#define RT_DEFER_REL 1
-#endif
 #ifndef RT_DEFER_THIN
 #define RT_DEFER_THIN 16
 #endif
@@ -1321,9 +1285,6 @@ __device__ __forceinline__ Node4Rows load_node4(const RT_LDS float4* nl, uint32_
 }
 #ifndef RT_SPHERE_RINV
 #define RT_SPHERE_RINV 1  // basic / mesh tiers: a static sphere's 1.0 / r from the flatten, not divided per hit
-#endif
-#ifndef RT_SORT_SKIP
-#define RT_SORT_SKIP 1
 #endif
 // visit4 on node rows already loaded; the ref row holds walk words (bword)
 template <class Stack>
@@ -1361,13 +1322,11 @@ __device__ __forceinline__ uint32_t visit4_rows(const SceneView& S, const Node4R
             key[i] = h ? e : INF;
         }
     }
-#if RT_SORT_SKIP
     // no lane of the wave hit a box child (nodes of spheres only, or every
     // box missed): nothing to sort or push (C2 -0.65 %, A/B at 128 spp, 5
     // reps, RMSE 0; a two-slot network when no lane has a box in slots 0 and
     // 1 was +1.9 %)
     if (!__ballot(fminf(fminf(key[0], key[1]), fminf(key[2], key[3])) < INF)) return 0u;
-#endif
     auto cs = [&](int a, int b) {  // compare-exchange: key[a] <= key[b] afterwards
         const bool sw = key[b] < key[a];
         const float ka = key[a], kb = key[b];
@@ -1471,13 +1430,9 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const bool can = (T.cur != 0u || T.sp > 0) && pn <= ROOM;
     const unsigned long long mw0 = __ballot(can);
     const unsigned long long mp0 = __ballot(pn > 0);
-#if RT_DEFER_REL
     const uint32_t in_walk = (uint32_t)__popcll(__ballot(true));
     const uint32_t thresh =
         in_walk <= RT_DEFER_THIN ? 1u : min((uint32_t)RT_DEFER_THRESH, (in_walk * 3u + 3u) / 4u);
-#else
-    constexpr uint32_t thresh = RT_DEFER_THRESH;
-#endif
     const bool round = (mw0 == 0 || (uint32_t)__popcll(mp0) >= thresh) && pn > 0;
     // the loads are unconditional (a lane without a round / a node reads
     // entry 0, cache-hot) so that no branch stands between them and their
@@ -1593,7 +1548,7 @@ __device__ Rec make_record(const SceneView& S, const Ray& wr, const HitInfo& h, 
         // them or an OBJ triangle's RemappedMaterial (obj.rs:32-62); nothing
         // else looks at them (full tiers: C3 -1.3 %, C5 -2 %; the mesh tier's
         // OBJ triangles always need them)
-        if (!RT_UV_ON_DEMAND || !FULL || (S.materials[rec.mat].flags & MF_NEEDS_UV) ||
+        if (!FULL || (S.materials[rec.mat].flags & MF_NEEDS_UV) ||
             (PLANAR && kind == K_TRI && S.planar_remap[idx] >= 0)) {
             const D3 hv = p - d3(P.f[4], P.f[5], P.f[6]);
             const D3 u = d3(P.f[7], P.f[8], P.f[9]), v = d3(P.f[10], P.f[11], P.f[12]), w = d3(P.f[13], P.f[14], P.f[15]);
@@ -1821,14 +1776,11 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
     return light_random_one(S, ref, o, rng, ovf, ok);
 }
 
-#ifndef RT_SOLID_ALBEDO
-#define RT_SOLID_ALBEDO 1
-#endif
 // A material's texture value; a SolidColor's colour comes with the material
 // record (MF_SOLID, set by the flatten), one dependent load fewer.
 template <bool FULL, bool PL = false>
 __device__ __forceinline__ D3 mat_tex(const SceneView& S, const DMaterial& M, double u, double v, D3 p) {
-    if (RT_SOLID_ALBEDO && (M.flags & MF_SOLID)) return d3(M.albedo[0], M.albedo[1], M.albedo[2]);
+    if (M.flags & MF_SOLID) return d3(M.albedo[0], M.albedo[1], M.albedo[2]);
     return tex_value<FULL, PL>(S, M.tex, u, v, p);
 }
 
@@ -1852,19 +1804,10 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
 struct Draws {
     double xi0, xi1, sn, cs;
 };
-// Tiers (bit 0 basic, bit 1 mesh) whose main loop shares the draws.  A/B
-// (RMSE 0): C2 -1.3 % (64 spp) / -1.8 % (128 spp) kernel time; the mesh tier
-// +3.3 % on C4 (64 spp): there the loop's extra live state spills 44 B/lane.
-#ifndef RT_UNIFIED_DRAWS
-#define RT_UNIFIED_DRAWS 1
-#endif
-// basic tier: in-walk restarts of missed / pathless lanes (0 = off; A/B)
-#ifndef RT_WALK_RESTART
-#define RT_WALK_RESTART 0
-#endif
-#ifndef RT_WALK_RESTART_MIN
-#define RT_WALK_RESTART_MIN 16
-#endif
+// The basic tier's main loop shares the draws.  A/B (RMSE 0): C2 -1.3 % (64
+// spp) / -1.8 % (128 spp) kernel time; the mesh tier +3.3 % on C4 (64 spp):
+// there the loop's extra live state spills 44 B/lane, so it keeps the loop of
+// the full tiers.
 
 // ---- general materials (tier FULL_GL): DiffuseLight / Mix wrappers nested
 // up to RT_MAT_DEPTH levels (rt_scene.cpp checks), Mix::from_image ratios.
@@ -2191,7 +2134,7 @@ struct KParams {
 template <int TIER>
 __device__ __forceinline__ StackFor<TIER> make_stack(RT_LDS uint2* s8, RT_LDS uint32_t* s4, RT_GLOBAL uint2* ovf,
                                                      uint32_t stride) {
-    if constexpr (TIER == TIER_BASIC && RT_STACK4B)
+    if constexpr (TIER == TIER_BASIC)
         return StackFor<TIER>{s4};
     else
         return StackFor<TIER>{s8, ovf, stride};
@@ -2207,15 +2150,15 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     uint32_t* queue = P->queue;
     constexpr int STACK = lds_stack_entries(TIER);
     constexpr uint32_t BLK = TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK;
-    constexpr bool B4 = TIER == TIER_BASIC && RT_STACK4B;
+    constexpr bool B4 = TIER == TIER_BASIC;
     // The lane arena (all tiers but the basic one): one uint2 row per lane and
     // row, RT_BLOCK apart -- the stack's rows, then (full tiers) the media
     // queue's (MedQ), then (full-flat tier) the parked path state's -- so
     // that every per-lane LDS access is one base address (threadIdx.x * 8)
     // plus a constant in the instruction's offset field, not a base VGPR per
     // array held across the path loop
-    constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT && RT_FLAT_LDS_STATE;
-    constexpr bool PARK_RAY = LDS_STATE && RT_FLAT_PARK_RAY;  // + the world ray (7 doubles)
+    constexpr bool LDS_STATE = TIER == TIER_FULL_FLAT;
+    constexpr bool PARK_RAY = LDS_STATE;  // + the world ray (7 doubles)
     constexpr uint32_t R_MED = B4 ? 0u : (uint32_t)STACK;
     constexpr uint32_t R_PST = R_MED + (tier_full(TIER) ? 2u * RT_MEDIA_CAP : 0u);
     constexpr uint32_t R_PIT = R_PST + (LDS_STATE ? (PARK_RAY ? 16u : 9u) : 0u);
@@ -2233,7 +2176,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     // words: cur, sp | pn | found, c, c_f, hit t, hit ref), so that the
     // shading code does not hold it in registers.
     constexpr bool PARK = (TIER == TIER_BASIC && RT_SHADE_BATCH_BASIC < 64) ||
-                          (TIER == TIER_MESH && RT_MESH_PARK && RT_SHADE_BATCH_MESH < 64);
+                          (TIER == TIER_MESH && RT_SHADE_BATCH_MESH < 64);
     __shared__ uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
     RT_LDS uint32_t* pk = (RT_LDS uint32_t*)(park_lds + threadIdx.x);
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
@@ -2406,7 +2349,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             need = true;
         }
     };
-    if constexpr (!tier_full(TIER) && ((RT_UNIFIED_DRAWS >> TIER) & 1)) {
+    if constexpr (TIER == TIER_BASIC) {
         // Basic / mesh tiers: a lane's iteration is walk -> (miss: the sample
         // ends) -> refill -> draws -> shade or a new sample's camera ray, so
         // that the one Philox block and sincos of the iteration's Draws serve
@@ -2435,7 +2378,6 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             vertex = 1;
             no_path = false;
         };
-        bool quit = false;  // RT_WALK_RESTART: the queue ran out for this lane inside a walk phase
         for (;;) {
             RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
 #ifdef RT_WAVE_TRACE
@@ -2460,44 +2402,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                     return trace_step<TIER>(S, ray, T, stk, rng, med, dg);
                 }
             };
-            if constexpr (BATCH >= 64 && TIER == TIER_BASIC && RT_WALK_RESTART > 0) {
-                // In-walk restarts (A/B): while the wave walks, lanes whose walk
-                // missed (the sample ends at the sky) or that hold no path start
-                // their next sample's camera ray at once, in rounds of at least
-                // RT_WALK_RESTART such lanes while at least RT_WALK_RESTART_MIN
-                // lanes still walk -- the walk phase's idle lanes take new walks
-                // instead of waiting for the wave's longest walk.  Same draws,
-                // same sums in s_j order: the same bits.
-                for (;;) {
-                    if (walking) walking = step();
-                    const unsigned long long wk = __ballot(walking);
-                    if (wk == 0) break;
-                    const bool restart = !walking && !quit && (no_path || !T.found);
-                    const unsigned long long rm = __ballot(restart);
-                    if ((uint32_t)__popcll(rm) < RT_WALK_RESTART || (uint32_t)__popcll(wk) < RT_WALK_RESTART_MIN)
-                        continue;
-                    if (restart && !no_path) {  // the miss: Environment::value, and the sample ends
-                        bool panic = false;
-                        shade<TIER>(S, ray, beta, L, rng, false, T.hit, panic);
-                        if (panic) ++n_panics;
-                        finish_sample();
-                        no_path = true;
-                    }
-                    if (!quit && !refill()) quit = true;  // the wave's pool: uniform control flow
-                    if (restart && !quit) {
-                        rng.sample = (sie & 0xFFFFu) * F.S + s_j;
-                        Draws Dr;
-                        rng.pair(0u, F.defocus ? 1u : 0u, Dr.xi0, Dr.xi1);
-                        k_sincos_2pi(Dr.xi0, &Dr.sn, &Dr.cs);
-                        camera_ray(Dr);
-                        rng.begin(vertex);
-                        ++n_rays;
-                        trace_begin<TIER>(S, ray, T);
-                        walking = true;
-                    }
-                }
-                if (quit) break;
-            } else if constexpr (BATCH >= 64) {
+            if constexpr (BATCH >= 64) {
 #ifdef RT_WAVE_TRACE
                 while (walking) walking = step(), ++trace_steps;
 #else
@@ -2759,7 +2664,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         }
         bool panic = false;
         Draws Dr{};
-        if constexpr (!tier_full(TIER)) {  // (RT_UNIFIED_DRAWS off: the shading draws made here)
+        if constexpr (!tier_full(TIER)) {  // (the mesh tier: the shading draws made here)
             if (T.found) {
                 uint32_t ovf = 0;
                 Dr.xi0 = rng.next(ovf);
@@ -3013,7 +2918,7 @@ __global__ void __launch_bounds__(256) rt_reduce_kernel(const double* __restrict
     if (srgb) srgb[(uint64_t)p * 3 + c] = srgb_u8(v, toon);
 }
 
-// The same sums, staged through LDS (RT_REDUCE_LDS): one wave per group of
+// The same sums, staged through LDS: one wave per group of
 // `pw` consecutive pixels of one region (whole rows: np = 1; tail rows: np =
 // parts; fine rows: np = parts2), whose part sums are contiguous in slot
 // order.  The wave copies the group's doubles into LDS with whole-line loads
@@ -3220,44 +3125,34 @@ static void fill_kparams(rtk::KParams& K, const rtk::SceneView* view, const rtk_
     K.stack_ovf = (RT_GLOBAL uint2*)stack_ovf;
 }
 
-#ifndef RT_REDUCE_LDS
-#define RT_REDUCE_LDS 1
-#endif
 static hipError_t launch_reduce(const rtk_frame_desc* fd, const rtk::Frame& F, double* partial, float* out,
                                 uint8_t* srgb, int toon, hipStream_t stream) {
     const uint32_t npix = fd->W * fd->rows;
-    if (RT_REDUCE_LDS) {
-        // the three regions of the slot order (rtk::Frame): whole rows, tail
-        // parts, fine parts; a region whose pixel does not fit the wave's LDS
-        // (S x np x 24 B > 16 KiB, e.g. C5's 64 x 16 tail parts) takes the
-        // direct kernel for the whole frame
-        const uint32_t whole_px = F.whole_items / fd->S, fine_px = F.fine_item0 / fd->S;
-        const struct { uint32_t b, e, np; } reg[3] = {
-            {0u, whole_px, 1u}, {whole_px, fine_px, F.parts}, {fine_px, npix, F.parts2}};
-        uint64_t slot = 0;
-        for (const auto& r : reg) {
-            if (r.e > r.b) {
-                const uint64_t dpp = (uint64_t)fd->S * r.np * 3u;  // doubles per pixel
-                if (dpp <= rtk::REDUCE_LDS_DOUBLES) {
-                    const uint32_t pw = (uint32_t)std::min<uint64_t>(64u, rtk::REDUCE_LDS_DOUBLES / dpp);
-                    const uint32_t groups = (r.e - r.b + pw - 1u) / pw;
-                    hipLaunchKernelGGL(rtk::rt_reduce_lds_kernel, dim3(groups), dim3(64), 0, stream, partial, r.b,
-                                       r.e, slot, fd->S, r.np, pw, fd->pixel_sample_scale, out, srgb, toon);
-                } else {
-                    const uint32_t waves = (r.e - r.b + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
-                    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, partial,
-                                       r.b, r.e, fd->S, F.parts, whole_px, F.parts2, fine_px,
-                                       fd->pixel_sample_scale, out, srgb, toon);
-                }
+    // the three regions of the slot order (rtk::Frame): whole rows, tail
+    // parts, fine parts; a region whose pixel does not fit the wave's LDS
+    // (S x np x 24 B > 16 KiB, e.g. C5's 64 x 16 tail parts) takes the
+    // direct kernel for that region
+    const uint32_t whole_px = F.whole_items / fd->S, fine_px = F.fine_item0 / fd->S;
+    const struct { uint32_t b, e, np; } reg[3] = {
+        {0u, whole_px, 1u}, {whole_px, fine_px, F.parts}, {fine_px, npix, F.parts2}};
+    uint64_t slot = 0;
+    for (const auto& r : reg) {
+        if (r.e > r.b) {
+            const uint64_t dpp = (uint64_t)fd->S * r.np * 3u;  // doubles per pixel
+            if (dpp <= rtk::REDUCE_LDS_DOUBLES) {
+                const uint32_t pw = (uint32_t)std::min<uint64_t>(64u, rtk::REDUCE_LDS_DOUBLES / dpp);
+                const uint32_t groups = (r.e - r.b + pw - 1u) / pw;
+                hipLaunchKernelGGL(rtk::rt_reduce_lds_kernel, dim3(groups), dim3(64), 0, stream, partial, r.b,
+                                   r.e, slot, fd->S, r.np, pw, fd->pixel_sample_scale, out, srgb, toon);
+            } else {
+                const uint32_t waves = (r.e - r.b + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
+                hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((waves + 3) / 4), dim3(256), 0, stream, partial,
+                                   r.b, r.e, fd->S, F.parts, whole_px, F.parts2, fine_px,
+                                   fd->pixel_sample_scale, out, srgb, toon);
             }
-            slot += (uint64_t)(r.e - r.b) * fd->S * r.np;
         }
-        return hipGetLastError();
+        slot += (uint64_t)(r.e - r.b) * fd->S * r.np;
     }
-    const uint32_t reduce_waves = (npix + rtk::REDUCE_PX_PER_WAVE - 1) / rtk::REDUCE_PX_PER_WAVE;
-    hipLaunchKernelGGL(rtk::rt_reduce_kernel, dim3((reduce_waves + 3) / 4), dim3(256), 0, stream, partial, 0u, npix, fd->S,
-                       F.parts, F.whole_items / fd->S, F.parts2, F.fine_item0 / fd->S, fd->pixel_sample_scale, out,
-                       srgb, toon);
     return hipGetLastError();
 }
 
