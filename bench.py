@@ -303,8 +303,9 @@ def cpu_baseline(threads, row_stride, spp, workload="c2", cpu_info=None):
             res["whole_host_estimated"]["lower_bound_basis"] = (
                 f"the same per-core rate scaled by base / max boost clock ({spec[0]} / {spec[1]} GHz, the part's "
                 "spec): every core of the loaded node at its guaranteed base clock, the measured cores at full boost "
-                "-- the most the all-core load can cost in clock (memory bandwidth is not this oracle's bound: its "
-                "working set is the 123-KB world)")
+                "-- the most the all-core load can cost in clock" +
+                (" (memory bandwidth is not this oracle's bound: C2's world is 123 KB)" if workload == "c2" else
+                 "; a memory-bound share of the work is not bounded"))
     if workload == "c2":
         s1 = rt.Scene(api)
         w1, l1, cam1 = scenes.random_spheres(s1, 400, 100)
