@@ -65,10 +65,15 @@ struct Diag {
     // (rth::bvh4_convert numbers the top levels first, breadth-first), and
     // node reads of lanes at those nodes (lane counts)
     unsigned long long u_top[4] = {0, 0, 0, 0}, l_top[4] = {0, 0, 0, 0}, l_node = 0;
+    // full tiers' shading rounds: rounds, lanes shaded, distinct shading
+    // classes per round (miss, Lambertian by texture kind, Metal, Dielectric,
+    // light, Isotropic, other) -- the branches a round executes one after the
+    // other whatever the order of its lanes
+    unsigned long long sh_rounds = 0, sh_lanes = 0, sh_classes = 0;
 #endif
 };
 #ifdef RT_DIAG
-constexpr int RT_DIAG_N = 33;
+constexpr int RT_DIAG_N = 36;
 __device__ unsigned long long g_diag[RT_DIAG_N];
 #define RT_DIAG_ONLY(x) x
 #else
@@ -2672,6 +2677,27 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 k_sincos_2pi(Dr.xi0, &Dr.sn, &Dr.cs);
             }
         }
+#ifdef RT_DIAG
+        {  // the round's shading classes (diagnostic build): one dependent load for the material
+            uint32_t cls = 0;  // miss
+            if (T.found) {
+                const uint32_t k = ref_kind(T.hit.ref), i = ref_index(T.hit.ref);
+                const int32_t m = k == K_SPHERE ? S.sphere_mat[i] : k == K_MSPHERE ? S.msph_mat[i]
+                                : (k == K_QUAD || k == K_TRI) ? S.planar_mat[i] : k == K_MEDIUM ? S.media[i].phase_mat : -1;
+                const int32_t mt = m >= 0 ? S.materials[m].type : -1;
+                cls = mt == M_LAMBERTIAN ? 1u + (uint32_t)min(S.textures[S.materials[m].tex].type, 4)
+                    : mt == M_METAL ? 6u : mt == M_DIELECTRIC ? 7u : mt == M_DIFFUSE_LIGHT ? 8u : mt == M_ISOTROPIC ? 9u : 10u;
+            }
+            const unsigned long long act = __ballot(true);
+            uint32_t kinds = 0;
+            for (uint32_t c = 0; c <= 10u; ++c) kinds += __ballot(cls == c) != 0ull ? 1u : 0u;
+            if (__lane_id() == (uint32_t)(__ffsll((long long)act) - 1)) {
+                ++dg.sh_rounds;
+                dg.sh_lanes += (unsigned long long)__popcll(act);
+                dg.sh_classes += kinds;
+            }
+        }
+#endif
         bool end_path = shade<TIER>(S, ray, beta, L, rng, T.found, T.hit, panic, Dr);
         RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_b1;)
         if (panic) {
@@ -2747,6 +2773,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         atomicAdd(&g_diag[28 + k], dg.l_top[k]);
     }
     atomicAdd(&g_diag[32], dg.l_node);
+    if (lane == 0) {
+        atomicAdd(&g_diag[33], dg.sh_rounds);
+        atomicAdd(&g_diag[34], dg.sh_lanes);
+        atomicAdd(&g_diag[35], dg.sh_classes);
+    }
 #endif
 #ifdef RT_WAVE_TRACE
     hist.flush();

@@ -37,7 +37,7 @@ elif wl == "c5":
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
-buf = (ctypes.c_ulonglong * 33)()
+buf = (ctypes.c_ulonglong * 36)()
 lib.rt_diag_counters(buf, 1)
 _, _, st = cam.render(world, lights, seed=1, want_srgb=False)
 lib.rt_diag_counters(buf, 0)
@@ -78,6 +78,12 @@ out = {
     # reads that are of those nodes (lane count)
     "top_uniform_step_share": {str(k): (c[24 + i] / c[16] if c[16] else None) for i, k in enumerate((5, 21, 85, 341))},
     "top_node_read_share": {str(k): (c[28 + i] / c[32] if c[32] else None) for i, k in enumerate((5, 21, 85, 341))},
-    "raw": c[:33],
+    # full tiers: shading rounds -- lanes per round and distinct shading
+    # classes per round (miss, Lambertian x texture kind, Metal, Dielectric,
+    # light, Isotropic, other): the branches a round runs one after another,
+    # the same whatever the order of the round's lanes
+    "shade_lanes_per_round": c[34] / c[33] if c[33] else None,
+    "shade_classes_per_round": c[35] / c[33] if c[33] else None,
+    "raw": c[:36],
 }
 print(json.dumps(out, indent=1))
