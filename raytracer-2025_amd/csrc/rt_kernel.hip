@@ -70,10 +70,13 @@ struct Diag {
     // light, Isotropic, other) -- the branches a round executes one after the
     // other whatever the order of its lanes
     unsigned long long sh_rounds = 0, sh_lanes = 0, sh_classes = 0;
+    // basic tier: wave iterations with no lane able to walk a node (pure
+    // sphere rounds), and the lanes with a queued sphere in them
+    unsigned long long pure_rounds = 0, pure_lanes = 0, pure_max_pn = 0;
 #endif
 };
 #ifdef RT_DIAG
-constexpr int RT_DIAG_N = 36;
+constexpr int RT_DIAG_N = 39;
 __device__ unsigned long long g_diag[RT_DIAG_N];
 #define RT_DIAG_ONLY(x) x
 #else
@@ -1439,6 +1442,17 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const uint32_t thresh =
         in_walk <= RT_DEFER_THIN ? 1u : min((uint32_t)RT_DEFER_THRESH, (in_walk * 3u + 3u) / 4u);
     const bool round = (mw0 == 0 || (uint32_t)__popcll(mp0) >= thresh) && pn > 0;
+#ifdef RT_DIAG
+    if (mw0 == 0 && __lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) {
+        ++dg.pure_rounds;
+        dg.pure_lanes += (unsigned long long)__popcll(mp0);
+    }
+    if (mw0 == 0) {  // the most spheres any lane of the wave still has queued
+        uint32_t mx = 0;
+        for (uint32_t k = 1; k <= RT_PEND_CAP; ++k) mx += __ballot(pn >= k) != 0ull ? 1u : 0u;
+        if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) dg.pure_max_pn += mx;
+    }
+#endif
     // the loads are unconditional (a lane without a round / a node reads
     // entry 0, cache-hot) so that no branch stands between them and their
     // waits: the sphere test then waits for its own load only
@@ -2777,6 +2791,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         atomicAdd(&g_diag[33], dg.sh_rounds);
         atomicAdd(&g_diag[34], dg.sh_lanes);
         atomicAdd(&g_diag[35], dg.sh_classes);
+        atomicAdd(&g_diag[36], dg.pure_rounds);
+        atomicAdd(&g_diag[37], dg.pure_lanes);
+        atomicAdd(&g_diag[38], dg.pure_max_pn);
     }
 #endif
 #ifdef RT_WAVE_TRACE

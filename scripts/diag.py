@@ -37,7 +37,7 @@ elif wl == "c5":
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
-buf = (ctypes.c_ulonglong * 36)()
+buf = (ctypes.c_ulonglong * 39)()
 lib.rt_diag_counters(buf, 1)
 _, _, st = cam.render(world, lights, seed=1, want_srgb=False)
 lib.rt_diag_counters(buf, 0)
@@ -84,6 +84,12 @@ out = {
     # the same whatever the order of the round's lanes
     "shade_lanes_per_round": c[34] / c[33] if c[33] else None,
     "shade_classes_per_round": c[35] / c[33] if c[33] else None,
-    "raw": c[:36],
+    # basic tier: wave iterations in which no lane can walk a node (pure
+    # sphere rounds: share of the walk's wave iterations), the lanes with a
+    # queued sphere in them, and the most any lane still had queued
+    "pure_sphere_round_share": c[36] / c[3] if c[3] else None,
+    "pure_round_lanes": c[37] / c[36] if c[36] else None,
+    "pure_round_max_queued": c[38] / c[36] if c[36] else None,
+    "raw": c[:39],
 }
 print(json.dumps(out, indent=1))

@@ -32,7 +32,7 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "c2"
     spp = int(sys.argv[2]) if len(sys.argv) > 2 else bench.WORKLOADS[wl][1]
     threads, _ = bench.usable_cpus()
-    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_fast.so")  # the timed build: the same bits as liboracle.so (tests/test_oracle_golden.py), faster
     if not os.path.exists(so):
         subprocess.run(["make", "-j", "8", "-C", os.path.join(ROOT, "oracle")], check=True, stdout=subprocess.DEVNULL)
     torch.cuda.init()
