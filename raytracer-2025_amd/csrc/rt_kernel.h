@@ -25,6 +25,11 @@
 // (sphere-count scaling)
 #define RT_NODE_LDS_BYTES 73696
 #endif
+#ifndef RT_NODE_LDS_BATCH_BYTES
+// basic tier with shading batches (trees of at most 365 nodes, C1 / C2: 241):
+// the node copy shrinks by the 32-KiB park area (8 words per lane)
+#define RT_NODE_LDS_BATCH_BYTES 40880
+#endif
 #ifndef RT_STACK_MESH
 // mesh tier: 16 entries = 32 KiB in LDS beside the 8-KiB park area (the walk
 // state of lanes whose walk carries over a shading batch: 8 words), 40 KiB

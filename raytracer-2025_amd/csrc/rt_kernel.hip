@@ -948,10 +948,18 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_MESH>& T, 
 }
 // Basic tier with shading batches: a carried-over walk's state is parked in
 // LDS across the shading round (the ray-derived fields are made again).
+#ifndef RT_PARK_INVA
+#define RT_PARK_INVA 0  // basic tier: park 1 / |d|^2 too (2 more words) instead of dividing again on resume
+#endif
 template <class Park>
 __device__ __forceinline__ void trace_park(const Trav<TIER_BASIC>& T, Park pk) {
     constexpr uint32_t B = RT_BLOCK_BASIC;
     const uint64_t c = (uint64_t)__double_as_longlong(T.cl.c), ht = (uint64_t)__double_as_longlong(T.hit.t);
+    if constexpr (RT_PARK_INVA) {
+        const uint64_t ia = (uint64_t)__double_as_longlong(T.inva);
+        pk[8 * B] = (uint32_t)ia;
+        pk[9 * B] = (uint32_t)(ia >> 32);
+    }
     pk[0 * B] = T.cur;
     pk[1 * B] = T.sp | (T.pn << 8) | ((uint32_t)T.found << 16);
     pk[2 * B] = (uint32_t)c;
@@ -975,7 +983,10 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_BASIC>& T,
     T.hit.ref = pk[7 * B];
     T.rf = make_rayf(wr);
     T.a = len2(wr.d);
-    T.inva = 1.0 / T.a;
+    if constexpr (RT_PARK_INVA)
+        T.inva = __hiloint2double((int)pk[9 * B], (int)pk[8 * B]);
+    else
+        T.inva = 1.0 / T.a;
     const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
     T.sf = make_sphf(o, d);
 }
@@ -1282,6 +1293,7 @@ struct Node4Rows {
     float4 lx, ly, lz, hx, hy, hz, rq;
 };
 constexpr uint32_t NODE_LDS_CAP = RT_NODE_LDS_BYTES / sizeof(DNode4);
+constexpr uint32_t NODE_LDS_CAP_BATCH = RT_NODE_LDS_BATCH_BYTES / sizeof(DNode4);
 // The node rows from the block's LDS copy: the launcher gives the basic tier
 // only worlds whose whole 4-wide tree fits it (NODE_LDS_CAP nodes: about 900
 // spheres; larger sphere worlds run the mesh tier).  A per-wave
@@ -2074,7 +2086,13 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
 // for C2 the shading divergence of small batches costs more than the walks
 // gain (A/B in DESIGN.md).
 #ifndef RT_SHADE_BATCH_BASIC
-#define RT_SHADE_BATCH_BASIC 64
+// basic tier over a tree of at most NODE_LDS_CAP_BATCH nodes (C1 / C2: 241):
+// shading in 56-lane batches, the carried-over walks parked in LDS (32 KiB
+// taken from the node copy).  Round 5, with the shared-draws loop: C2 -2.3 %
+// kernel time against whole-wave shading (A/B at 128 spp, RMSE 0; round 2's
+// loop had measured +1.7 %).  Larger trees (up to NODE_LDS_CAP) run the
+// whole-wave variant of the tier (rt_path_kernel<TIER_BASIC, true>).
+#define RT_SHADE_BATCH_BASIC 56
 #endif
 #ifndef RT_SHADE_BATCH_MESH
 #define RT_SHADE_BATCH_MESH 48
@@ -2158,11 +2176,17 @@ __device__ __forceinline__ StackFor<TIER> make_stack(RT_LDS uint2* s8, RT_LDS ui
     else
         return StackFor<TIER>{s8, ovf, stride};
 }
-constexpr uint32_t RT_PARK_WORDS = 8;
+constexpr uint32_t RT_PARK_WORDS = 8 + 2 * RT_PARK_INVA;
 
-template <int TIER>
+// WIDE (basic tier only): the variant for trees of NODE_LDS_CAP_BATCH +
+// 1 .. NODE_LDS_CAP nodes -- the whole LDS node copy, whole-wave shading, no
+// park area.
+template <int TIER, bool WIDE = false>
 __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK, TIER == TIER_FULL_FLAT ? RT_FLAT_WAVES : tier_full_bvh(TIER) ? RT_FULL_WAVES : (TIER == TIER_MESH ? RT_MESH_WAVES : RT_BASIC_WAVES))
     rt_path_kernel(const KParams* __restrict__ P) {
+    static_assert(!WIDE || TIER == TIER_BASIC, "the wide variant is the basic tier's");
+    constexpr int BASIC_BATCH = WIDE ? 64 : RT_SHADE_BATCH_BASIC;
+    constexpr uint32_t NODE_CAP = WIDE ? NODE_LDS_CAP : NODE_LDS_CAP_BATCH;
     // The params block is read-only for the launch: scalar loads, hoisted.
     const SceneView S = P->S;
     const Frame& F = P->F;
@@ -2194,15 +2218,15 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     // carries over a shading round is parked here across it (RT_PARK_WORDS
     // words: cur, sp | pn | found, c, c_f, hit t, hit ref), so that the
     // shading code does not hold it in registers.
-    constexpr bool PARK = (TIER == TIER_BASIC && RT_SHADE_BATCH_BASIC < 64) ||
+    constexpr bool PARK = (TIER == TIER_BASIC && BASIC_BATCH < 64) ||
                           (TIER == TIER_MESH && RT_SHADE_BATCH_MESH < 64);
     __shared__ uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
     RT_LDS uint32_t* pk = (RT_LDS uint32_t*)(park_lds + threadIdx.x);
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
     // 241 nodes for C1/C2), read by every node visit instead of global memory.
-    __shared__ float4 node_lds[TIER == TIER_BASIC && RT_BVH4 ? NODE_LDS_CAP * 7 : 1];
+    __shared__ float4 node_lds[TIER == TIER_BASIC && RT_BVH4 ? NODE_CAP * 7 : 1];
     if constexpr (TIER == TIER_BASIC && RT_BVH4) {
-        const uint32_t n_lds = min(S.n_nodes4, NODE_LDS_CAP);  // == n_nodes4 (launcher)
+        const uint32_t n_lds = min(S.n_nodes4, NODE_CAP);  // == n_nodes4 (launcher: rtk_launch_frame)
         const RT_GLOBAL float4* src = reinterpret_cast<const RT_GLOBAL float4*>(S.nodes4);
         for (uint32_t k = threadIdx.x; k < n_lds * 7u; k += BLK) {
             float4 v = src[k];
@@ -2375,7 +2399,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         // both (struct Draws).  A lane whose path ends in shading (depth,
         // panic, no scatter) starts its next sample one iteration later.
         bool no_path = true;  // the lane starts a sample at its next post-walk stage
-        constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC : RT_SHADE_BATCH_MESH;
+        constexpr int BATCH = TIER == TIER_BASIC ? BASIC_BATCH : RT_SHADE_BATCH_MESH;
         // ---- Camera::get_ray (camera.rs:247-273), vertex 0, from the iteration's draws
         auto camera_ray = [&](const Draws& Dr) {
             const uint32_t s_i = sie & 0xFFFFu, py = udiv_inv(rng.pixel, F.inv_W), px = rng.pixel - py * F.W;
@@ -2619,7 +2643,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             trace_unpark(ray, T, pk);  // a walk carried over the last shading round
         }
         RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
-        constexpr int BATCH = TIER == TIER_BASIC ? RT_SHADE_BATCH_BASIC
+        constexpr int BATCH = TIER == TIER_BASIC ? BASIC_BATCH
                             : TIER == TIER_MESH ? RT_SHADE_BATCH_MESH
                             : TIER == TIER_FULL ? RT_SHADE_BATCH_FULL : RT_SHADE_BATCH_FLAT;
         auto step = [&]() -> bool {
@@ -2848,6 +2872,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
 #if !defined(RT_COMMON_ONLY)
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 0
 RT_TIER_ENTRY(0)
+// the basic tier's wide variant (trees past NODE_LDS_CAP_BATCH nodes)
+extern "C" hipError_t rtk_launch_path_0w(int grid, hipStream_t stream, const rtk::KParams* P) {
+    hipLaunchKernelGGL((rtk::rt_path_kernel<0, true>), dim3(grid), dim3(RT_BLOCK_BASIC), 0, stream, P);
+    return hipGetLastError();
+}
 #endif
 #if !defined(RT_TIER_ONLY) || RT_TIER_ONLY == 1
 RT_TIER_ENTRY(1)
@@ -2902,6 +2931,7 @@ extern "C" int rt_diag_counters(unsigned long long* out, int reset) {
 
 #if !defined(RT_TIER_ONLY)
 extern "C" hipError_t rtk_launch_path_0(int, hipStream_t, const rtk::KParams*);
+extern "C" hipError_t rtk_launch_path_0w(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_1(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_2(int, hipStream_t, const rtk::KParams*);
 extern "C" hipError_t rtk_launch_path_3(int, hipStream_t, const rtk::KParams*);
@@ -3217,7 +3247,10 @@ extern "C" hipError_t rtk_launch_frame(const rtk::SceneView* view, const rtk_fra
     e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (fd->ev_start) (void)hipEventRecord((hipEvent_t)fd->ev_start, stream);
-    e = tier == rtk::TIER_BASIC  ? rtk_launch_path_0(grid, stream, Pd)
+    // the basic tier: shading batches over trees that leave room for the
+    // park area, whole-wave shading over the rest (rt_path_kernel WIDE)
+    e = tier == rtk::TIER_BASIC  ? (view->n_nodes4 > rtk::NODE_LDS_CAP_BATCH ? rtk_launch_path_0w(grid, stream, Pd)
+                                                                            : rtk_launch_path_0(grid, stream, Pd))
         : tier == rtk::TIER_MESH ? rtk_launch_path_1(grid, stream, Pd)
         : tier == rtk::TIER_FULL ? rtk_launch_path_2(grid, stream, Pd)
         : tier == rtk::TIER_FULL_FLAT ? rtk_launch_path_3(grid, stream, Pd)
