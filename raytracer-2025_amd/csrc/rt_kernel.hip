@@ -2392,7 +2392,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             need = true;
         }
     };
-    if constexpr (TIER == TIER_BASIC) {
+#ifndef RT_MESH_SHARED_DRAWS
+#define RT_MESH_SHARED_DRAWS 0  // A/B: the mesh tier in the shared-draws loop too (round 4: +3.3 % on C4, spills)
+#endif
+    if constexpr (TIER == TIER_BASIC || (TIER == TIER_MESH && RT_MESH_SHARED_DRAWS)) {
         // Basic / mesh tiers: a lane's iteration is walk -> (miss: the sample
         // ends) -> refill -> draws -> shade or a new sample's camera ray, so
         // that the one Philox block and sincos of the iteration's Draws serve
