@@ -1836,9 +1836,9 @@ struct Draws {
     double xi0, xi1, sn, cs;
 };
 // The basic tier's main loop shares the draws.  A/B (RMSE 0): C2 -1.3 % (64
-// spp) / -1.8 % (128 spp) kernel time; the mesh tier +3.3 % on C4 (64 spp):
-// there the loop's extra live state spills 44 B/lane, so it keeps the loop of
-// the full tiers.
+// spp) / -1.8 % (128 spp) kernel time; the mesh tier +3.3 % on C4 (64 spp,
+// round 4: the loop's extra live state spills 44 B/lane) and +1.0 % in round
+// 5 (28 B/lane), so it keeps the loop of the full tiers.
 
 // ---- general materials (tier FULL_GL): DiffuseLight / Mix wrappers nested
 // up to RT_MAT_DEPTH levels (rt_scene.cpp checks), Mix::from_image ratios.
@@ -2392,10 +2392,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             need = true;
         }
     };
-#ifndef RT_MESH_SHARED_DRAWS
-#define RT_MESH_SHARED_DRAWS 0  // A/B: the mesh tier in the shared-draws loop too (round 4: +3.3 % on C4, spills)
-#endif
-    if constexpr (TIER == TIER_BASIC || (TIER == TIER_MESH && RT_MESH_SHARED_DRAWS)) {
+    if constexpr (TIER == TIER_BASIC) {
         // Basic / mesh tiers: a lane's iteration is walk -> (miss: the sample
         // ends) -> refill -> draws -> shade or a new sample's camera ray, so
         // that the one Philox block and sincos of the iteration's Draws serve
