@@ -274,16 +274,22 @@ __device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double 
     return (double)px[3];
 }
 
+#ifndef RT_SKY_Y
+#define RT_SKY_Y 1  // basic / mesh tiers: a miss under a sky gradient makes only the unit direction's y
+#endif
+// the sky gradient (rt_tex_sky_gradient, include/rt_mi355x.h) at the unit direction's y
+__device__ __forceinline__ D3 sky_value(const DTexture& t, double py) {
+    const double a = 0.5 * (py + 1.0);
+    return (1.0 - a) * d3(t.color[0], t.color[1], t.color[2]) + a * d3(t.color2[0], t.color2[1], t.color2[2]);
+}
+
 template <bool FULL, bool PL = false>  // PL: NoiseTexture reads the LDS copy of the first Perlin table
 __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
     for (int guard = 0; guard < 16; ++guard) {
         const DTexture& t = S.textures[tid];
         switch (t.type) {
             case T_SOLID: return d3(t.color[0], t.color[1], t.color[2]);
-            case T_SKY: {
-                const double a = 0.5 * (p.y + 1.0);
-                return (1.0 - a) * d3(t.color[0], t.color[1], t.color[2]) + a * d3(t.color2[0], t.color2[1], t.color2[2]);
-            }
+            case T_SKY: return sky_value(t, p.y);
             case T_CHECKER: {
                 const int32_t xi = (int32_t)floor(t.scale * p.x), yi = (int32_t)floor(t.scale * p.y),
                               zi = (int32_t)floor(t.scale * p.z);
@@ -1902,6 +1908,21 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     uint32_t ovf = 0;
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
+        if constexpr (!FULL && RT_SKY_Y) {
+            // Basic / mesh tiers under a sky gradient (the world's background
+            // is wave-uniform: a scalar branch): the gradient reads the unit
+            // direction's y only, so only that quotient is made.  `ok` is the
+            // same as unit()'s finite3 of the three quotients: with l =
+            // |d| not NaN and not 0 and every component finite, each d_i / l
+            // is finite (|d_i| <= l, or l = inf over finite components: 0);
+            // l = 0 or NaN, or an infinite component (inf / inf), gives a NaN
+            if (S.background_tex >= 0 && S.textures[S.background_tex].type == T_SKY) {
+                const double l = len(ray.d);
+                if (isnan(l) || l == 0.0 || !finite3(ray.d)) panic = true;
+                L = L + beta * sky_value(S.textures[S.background_tex], ray.d.y / l);
+                return true;
+            }
+        }
         if (S.background_tex >= 0) {
             bool ok;
             const D3 p = unit(ray.d, ok);
