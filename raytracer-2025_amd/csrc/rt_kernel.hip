@@ -274,6 +274,9 @@ __device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double 
     return (double)px[3];
 }
 
+#ifndef RT_DEFINE_T
+#define RT_DEFINE_T 1  // basic tier: the walk state set up for lanes without a path too (see the main loop)
+#endif
 #ifndef RT_SKY_Y
 #define RT_SKY_Y 1  // basic tier: a miss under a sky gradient makes only the unit direction's y
 // (C2 -1.4 %; the mesh tier measured +0.4 % on C4 with it and keeps unit())
@@ -2474,12 +2477,15 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 // a new walk and a walk carried over the last shading round
                 // make the same ray-derived fields: once, for both (as two
                 // branches the wave ran that code twice in most rounds: C2
-                // -0.7 %, A/B at 128 spp, 5 reps, RMSE 0)
-                if (!no_path) {
+                // -0.7 %, A/B at 128 spp, 5 reps, RMSE 0).
+                // RT_DEFINE_T: a lane with no path (it starts its sample
+                // after this walk phase) sets up the walk state too, which it
+                // does not walk: the state is then defined on every path into
+                // the walk, so that the compiler need not keep the last
+                // walk's values live through the shading code
+                if (RT_DEFINE_T || !no_path) {
                     trace_ray_fields(ray, T);
                     if (!walking) {
-                        rng.begin(vertex);
-                        ++n_rays;
                         T.cl.c = __builtin_huge_val();
                         T.cl.c_f = __builtin_huge_valf();
                         T.sp = 0;
@@ -2489,7 +2495,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                         T.hit.nxf = 0;
                         T.nmed = 0;
                         T.cur = bword(S, S.world_root);
-                        walking = true;
+                        if (!no_path) {
+                            rng.begin(vertex);
+                            ++n_rays;
+                            walking = true;
+                        }
                     } else {
                         trace_unpark_state(T, pk);
                     }
