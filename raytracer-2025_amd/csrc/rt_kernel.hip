@@ -2482,7 +2482,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 // after this walk phase) sets up the walk state too, which it
                 // does not walk: the state is then defined on every path into
                 // the walk, so that the compiler need not keep the last
-                // walk's values live through the shading code
+                // walk's values live through the shading code (C2 -1.6 %:
+                // 28 B/lane of scratch -> none, 128 -> 124 VGPRs; A/B at 128
+                // spp, 5 reps, RMSE 0)
                 if (RT_DEFINE_T || !no_path) {
                     trace_ray_fields(ray, T);
                     if (!walking) {
