@@ -7,7 +7,10 @@ every render, e.g. RT_TAIL_PERMILLE=250).
   python scripts/tail_ab.py workload spp reps setting [setting ...]
 Prints per setting the frame's kernel ms (min, median) and the worst shard's
 (min over reps of the per-rep worst), and the 8-GPU kernel efficiency
-full / (8 x worst shard) from the minima."""
+full / (8 x worst shard) from the minima.
+TAIL_ORDER=rev renders the shards 7 .. 0 (shards_ms stays indexed by shard);
+TAIL_WARM=1 renders one untimed shard first, so that no timed shard follows
+the whole frame directly (a rank of an 8-GPU run renders only its shard)."""
 import importlib
 import json
 import os
@@ -46,10 +49,13 @@ def main():
                 ref = lin
             rel = float(abs(lin.astype("float64") - ref).max())  # settings may change f64 sum order: ~1 ulp
             res[k]["full"].append(st.kernel_ms)
-            shards = []
-            for r in range(8):
+            shards = [0.0] * 8
+            if os.environ.get("TAIL_WARM") == "1":
+                cam.render(world, lights, seed=1, row_offset=7, row_stride=8, want_srgb=False)
+            order = range(7, -1, -1) if os.environ.get("TAIL_ORDER") == "rev" else range(8)
+            for r in order:
                 _, _, st8 = cam.render(world, lights, seed=1, row_offset=r, row_stride=8, want_srgb=False)
-                shards.append(st8.kernel_ms)
+                shards[r] = st8.kernel_ms
             worst = max(shards)
             res[k]["worst8"].append(worst)
             res[k]["sum8"].append(sum(shards))
