@@ -274,13 +274,6 @@ __device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double 
     return (double)px[3];
 }
 
-#ifndef RT_DEFINE_T
-#define RT_DEFINE_T 1  // basic tier: the walk state set up for lanes without a path too (see the main loop)
-#endif
-#ifndef RT_SKY_Y
-#define RT_SKY_Y 1  // basic tier: a miss under a sky gradient makes only the unit direction's y
-// (C2 -1.4 %; the mesh tier measured +0.4 % on C4 with it and keeps unit())
-#endif
 // the sky gradient (rt_tex_sky_gradient, include/rt_mi355x.h) at the unit direction's y
 __device__ __forceinline__ D3 sky_value(const DTexture& t, double py) {
     const double a = 0.5 * (py + 1.0);
@@ -958,18 +951,10 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_MESH>& T, 
 }
 // Basic tier with shading batches: a carried-over walk's state is parked in
 // LDS across the shading round (the ray-derived fields are made again).
-#ifndef RT_PARK_INVA
-#define RT_PARK_INVA 0  // basic tier: park 1 / |d|^2 too (2 more words) instead of dividing again on resume
-#endif
 template <class Park>
 __device__ __forceinline__ void trace_park(const Trav<TIER_BASIC>& T, Park pk) {
     constexpr uint32_t B = RT_BLOCK_BASIC;
     const uint64_t c = (uint64_t)__double_as_longlong(T.cl.c), ht = (uint64_t)__double_as_longlong(T.hit.t);
-    if constexpr (RT_PARK_INVA) {
-        const uint64_t ia = (uint64_t)__double_as_longlong(T.inva);
-        pk[8 * B] = (uint32_t)ia;
-        pk[9 * B] = (uint32_t)(ia >> 32);
-    }
     pk[0 * B] = T.cur;
     pk[1 * B] = T.sp | (T.pn << 8) | ((uint32_t)T.found << 16);
     pk[2 * B] = (uint32_t)c;
@@ -998,27 +983,6 @@ __device__ __forceinline__ void trace_ray_fields(const Ray& wr, Trav<TIER_BASIC>
     T.rf = make_rayf(wr);
     T.a = len2(wr.d);
     T.inva = 1.0 / T.a;
-    const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
-    T.sf = make_sphf(o, d);
-}
-template <class Park>
-__device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_BASIC>& T, Park pk) {
-    constexpr uint32_t B = RT_BLOCK_BASIC;
-    T.cur = pk[0 * B];
-    const uint32_t w = pk[1 * B];
-    T.sp = w & 0xffu;
-    T.pn = (w >> 8) & 0xffu;
-    T.found = (w >> 16) & 1u;
-    T.cl.c = __hiloint2double((int)pk[3 * B], (int)pk[2 * B]);
-    T.cl.c_f = __uint_as_float(pk[4 * B]);
-    T.hit.t = __hiloint2double((int)pk[6 * B], (int)pk[5 * B]);
-    T.hit.ref = pk[7 * B];
-    T.rf = make_rayf(wr);
-    T.a = len2(wr.d);
-    if constexpr (RT_PARK_INVA)
-        T.inva = __hiloint2double((int)pk[9 * B], (int)pk[8 * B]);
-    else
-        T.inva = 1.0 / T.a;
     const double o[3] = {wr.o.x, wr.o.y, wr.o.z}, d[3] = {wr.d.x, wr.d.y, wr.d.z};
     T.sf = make_sphf(o, d);
 }
@@ -1912,7 +1876,9 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
     uint32_t ovf = 0;
     if (!hit_any) {
         // miss: Environment::value (environment.rs:14-24)
-        if constexpr (TIER == TIER_BASIC && RT_SKY_Y) {
+        if constexpr (TIER == TIER_BASIC) {
+            // (C2 -1.4 %, profiles/r05/ab_sky_y_c2_128spp.json; the mesh tier
+            // measured +0.4 % on C4 with it and keeps unit())
             // Basic tier under a sky gradient (the world's background
             // is wave-uniform: a scalar branch): the gradient reads the unit
             // direction's y only, so only that quotient is made.  `ok` is the
@@ -2223,7 +2189,7 @@ __device__ __forceinline__ StackFor<TIER> make_stack(RT_LDS uint2* s8, RT_LDS ui
     else
         return StackFor<TIER>{s8, ovf, stride};
 }
-constexpr uint32_t RT_PARK_WORDS = 8 + 2 * RT_PARK_INVA;
+constexpr uint32_t RT_PARK_WORDS = 8;
 
 // WIDE (basic tier only): the variant for trees of NODE_LDS_CAP_BATCH +
 // 1 .. NODE_LDS_CAP nodes -- the whole LDS node copy, whole-wave shading, no
@@ -2477,44 +2443,37 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 // a new walk and a walk carried over the last shading round
                 // make the same ray-derived fields: once, for both (as two
                 // branches the wave ran that code twice in most rounds: C2
-                // -0.7 %, A/B at 128 spp, 5 reps, RMSE 0).
-                // RT_DEFINE_T: a lane with no path (it starts its sample
-                // after this walk phase) sets up the walk state too, which it
-                // does not walk: the state is then defined on every path into
-                // the walk, so that the compiler need not keep the last
-                // walk's values live through the shading code (C2 -1.6 %:
-                // 28 B/lane of scratch -> none, 128 -> 124 VGPRs; A/B at 128
-                // spp, 5 reps, RMSE 0)
-                if (RT_DEFINE_T || !no_path) {
-                    trace_ray_fields(ray, T);
-                    if (!walking) {
-                        T.cl.c = __builtin_huge_val();
-                        T.cl.c_f = __builtin_huge_valf();
-                        T.sp = 0;
-                        T.found = false;
-                        T.pn = 0;
-                        T.nxf = 0;
-                        T.hit.nxf = 0;
-                        T.nmed = 0;
-                        T.cur = bword(S, S.world_root);
-                        if (!no_path) {
-                            rng.begin(vertex);
-                            ++n_rays;
-                            walking = true;
-                        }
-                    } else {
-                        trace_unpark_state(T, pk);
-                    }
-                }
-            } else if (!no_path) {
+                // -0.7 %, profiles/r05/ab_shared_rayfields_c2_128spp.json).
+                // A lane with no path (it starts its sample after this walk
+                // phase) sets up the walk state too, which it does not walk:
+                // the state is then defined on every path into the walk, so
+                // that the compiler need not keep the last walk's values live
+                // through the shading code (C2 -1.6 %: 28 B/lane of scratch
+                // -> none, 128 -> 124 VGPRs; ab_define_t_c2_128spp.json)
+                trace_ray_fields(ray, T);
                 if (!walking) {
-                    rng.begin(vertex);
-                    ++n_rays;
-                    trace_begin<TIER>(S, ray, T);
-                    walking = true;
-                } else if constexpr (PARK) {
-                    trace_unpark(ray, T, pk);  // a walk carried over the last shading round
+                    T.cl.c = __builtin_huge_val();
+                    T.cl.c_f = __builtin_huge_valf();
+                    T.sp = 0;
+                    T.found = false;
+                    T.pn = 0;
+                    T.nxf = 0;
+                    T.hit.nxf = 0;
+                    T.nmed = 0;
+                    T.cur = bword(S, S.world_root);
+                    if (!no_path) {
+                        rng.begin(vertex);
+                        ++n_rays;
+                        walking = true;
+                    }
+                } else {
+                    trace_unpark_state(T, pk);
                 }
+            } else if (!no_path && !walking) {  // the whole-wave variant: every walk ends in the walk phase
+                rng.begin(vertex);
+                ++n_rays;
+                trace_begin<TIER>(S, ray, T);
+                walking = true;
             }
             RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
             auto step = [&]() -> bool {
