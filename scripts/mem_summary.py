@@ -50,6 +50,10 @@ def main(rnd="r03", src="gpurun_out/mem"):
                             "per-XCD GRBM_GUI_ACTIVE as the cycle base; TCP/TD sums over 256 CUs"}
     dst = os.path.join(ROOT, "profiles", rnd, "mem")
     os.makedirs(dst, exist_ok=True)
+    old = os.path.join(dst, "mem_summary.json")
+    if os.path.exists(old):  # workloads this run did not measure keep theirs
+        prev = json.load(open(old))
+        out = {**{w: v for w, v in prev.items() if w not in out}, **out}
     json.dump(out, open(os.path.join(dst, "mem_summary.json"), "w"), indent=1)
     print(json.dumps({w: v["derived"] for w, v in out.items()}, indent=1))
 
