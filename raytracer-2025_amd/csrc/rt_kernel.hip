@@ -950,34 +950,30 @@ __device__ __forceinline__ void trace_unpark(const Ray& wr, Trav<TIER_MESH>& T, 
     T.inva = 1.0 / T.a;
 }
 // Basic tier with shading batches: a carried-over walk's state is parked in
-// LDS across the shading round (the ray-derived fields are made again).
-template <class Park>
-__device__ __forceinline__ void trace_park(const Trav<TIER_BASIC>& T, Park pk) {
+// LDS across the shading round as four 8-byte rows -- {cur, sp | pn | found},
+// c, {c_f, hit ref}, hit t: two ds_write2st64_b64 / ds_read2st64_b64 a park
+// and a resume, not four of the 4-byte kind (C2 -0.2 %, A/B at 128 spp, 5
+// reps, RMSE 0: profiles/r05/ab_park64_c2_128spp.json).  The ray-derived
+// fields are made again on resume (trace_ray_fields), as for a new walk.
+__device__ __forceinline__ void trace_park2(const Trav<TIER_BASIC>& T, RT_LDS uint2* pk) {
     constexpr uint32_t B = RT_BLOCK_BASIC;
     const uint64_t c = (uint64_t)__double_as_longlong(T.cl.c), ht = (uint64_t)__double_as_longlong(T.hit.t);
-    pk[0 * B] = T.cur;
-    pk[1 * B] = T.sp | (T.pn << 8) | ((uint32_t)T.found << 16);
-    pk[2 * B] = (uint32_t)c;
-    pk[3 * B] = (uint32_t)(c >> 32);
-    pk[4 * B] = __float_as_uint(T.cl.c_f);
-    pk[5 * B] = (uint32_t)ht;
-    pk[6 * B] = (uint32_t)(ht >> 32);
-    pk[7 * B] = T.hit.ref;
+    pk[0 * B] = make_uint2(T.cur, T.sp | (T.pn << 8) | ((uint32_t)T.found << 16));
+    pk[1 * B] = make_uint2((uint32_t)c, (uint32_t)(c >> 32));
+    pk[2 * B] = make_uint2(__float_as_uint(T.cl.c_f), T.hit.ref);
+    pk[3 * B] = make_uint2((uint32_t)ht, (uint32_t)(ht >> 32));
 }
-// The basic tier's resume in two halves: the walk state
-// from the park area, and the ray-derived fields, which a new walk makes too
-template <class Park>
-__device__ __forceinline__ void trace_unpark_state(Trav<TIER_BASIC>& T, Park pk) {
+__device__ __forceinline__ void trace_unpark_state2(Trav<TIER_BASIC>& T, const RT_LDS uint2* pk) {
     constexpr uint32_t B = RT_BLOCK_BASIC;
-    T.cur = pk[0 * B];
-    const uint32_t w = pk[1 * B];
-    T.sp = w & 0xffu;
-    T.pn = (w >> 8) & 0xffu;
-    T.found = (w >> 16) & 1u;
-    T.cl.c = __hiloint2double((int)pk[3 * B], (int)pk[2 * B]);
-    T.cl.c_f = __uint_as_float(pk[4 * B]);
-    T.hit.t = __hiloint2double((int)pk[6 * B], (int)pk[5 * B]);
-    T.hit.ref = pk[7 * B];
+    const uint2 w0 = pk[0 * B], w1 = pk[1 * B], w2 = pk[2 * B], w3 = pk[3 * B];
+    T.cur = w0.x;
+    T.sp = w0.y & 0xffu;
+    T.pn = (w0.y >> 8) & 0xffu;
+    T.found = (w0.y >> 16) & 1u;
+    T.cl.c = __hiloint2double((int)w1.y, (int)w1.x);
+    T.cl.c_f = __uint_as_float(w2.x);
+    T.hit.ref = w2.y;
+    T.hit.t = __hiloint2double((int)w3.y, (int)w3.x);
 }
 __device__ __forceinline__ void trace_ray_fields(const Ray& wr, Trav<TIER_BASIC>& T) {
     T.rf = make_rayf(wr);
@@ -2233,8 +2229,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     // shading code does not hold it in registers.
     constexpr bool PARK = (TIER == TIER_BASIC && BASIC_BATCH < 64) ||
                           (TIER == TIER_MESH && RT_SHADE_BATCH_MESH < 64);
-    __shared__ uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t park_lds[PARK ? RT_PARK_WORDS * BLK : 1];
     RT_LDS uint32_t* pk = (RT_LDS uint32_t*)(park_lds + threadIdx.x);
+    RT_LDS uint2* pk2 = (RT_LDS uint2*)park_lds + threadIdx.x;  // basic tier: 8-byte rows (trace_park2)
     // Basic tier: the block's copy of the world's 4-wide nodes (the whole tree:
     // 241 nodes for C1/C2), read by every node visit instead of global memory.
     __shared__ float4 node_lds[TIER == TIER_BASIC && RT_BVH4 ? NODE_CAP * 7 : 1];
@@ -2467,7 +2464,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                         walking = true;
                     }
                 } else {
-                    trace_unpark_state(T, pk);
+                    trace_unpark_state2(T, pk2);
                 }
             } else if (!no_path && !walking) {  // the whole-wave variant: every walk ends in the walk phase
                 rng.begin(vertex);
@@ -2499,14 +2496,14 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 }
             }
             RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
-            // a walk that carries over this shading round (mesh tier) is parked;
+            // a walk that carries over this shading round is parked;
             // the lane skips the rest of the iteration but for the refill,
             // which every lane of the wave runs: the queue pool (pool_next,
             // pool_end, dry) is wave-uniform state and must be updated in
             // uniform control flow, or a parked lane would keep a stale copy
             const bool carry = BATCH < 64 && walking;
             if constexpr (PARK) {
-                if (carry) trace_park(T, pk);
+                if (carry) trace_park2(T, pk2);
             }
             // ---- this lane's walk is over, or it has no path
             bool cam = no_path;
