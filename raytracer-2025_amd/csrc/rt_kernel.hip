@@ -1436,9 +1436,9 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     RT_DIAG_ONLY(if (__lane_id() == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) ++dg.wave_trace_iters;)
     uint32_t pn = T.pn;
     // The sphere round is decided on the state before this step's node
-    // round and issued first: its sphere load goes out before the node's
-    // seven loads (loads complete in order), and its f64 test runs while the
-    // node is in flight.
+    // round and its sphere load issued first, ahead of the node's seven LDS
+    // reads; its f64 test comes after the node visit, by when the load has
+    // landed.
     const bool can = (T.cur != 0u || T.sp > 0) && pn <= ROOM;
     const unsigned long long mw0 = __ballot(can);
     const unsigned long long mp0 = __ballot(pn > 0);
@@ -1484,18 +1484,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     const uint32_t r16 = cur >> 16;
     const bool node = r16 - 1u < 0x7fffu;  // 1 ..= 0x7fff
     const Node4Rows rows = load_node4(nl - 7, node ? r16 : 1u);
-    if (round) {  // sphere round (sphere.rs:77-108)
-        RT_DIAG_ONLY(++dg.sphere_tests;)
-        double t;
-        RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_tests;)
-        if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
-            RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_hits;)
-            T.cl.lower(t);
-            T.found = true;
-            T.hit.t = t;
-            T.hit.ref = make_ref(K_SPHERE, sidx);
-        }
-    }
+
     if (__ballot(!node && cur != 0u)) {  // lists, standalone spheres (none in C2)
         if (r16 >= 0x8000u) {  // a list position
             const uint32_t li = r16 & 0x7fffu;
@@ -1512,6 +1501,23 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     if (node) {
         RT_DIAG_ONLY(++dg.node_visits;)
         T.cur = visit4_rows(S, rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
+    }
+    // the sphere round's f64 test after the node visit: the visit's LDS rows
+    // arrive before the sphere's global load, and the test then finds it
+    // there (C2 -0.2 %, profiles/r05/ab_round_late_c2_128spp.json; the
+    // visit culls against the closest t before this test, which only makes
+    // it cull less, never wrongly)
+    if (round) {  // sphere round (sphere.rs:77-108)
+        RT_DIAG_ONLY(++dg.sphere_tests;)
+        double t;
+        RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_tests;)
+        if (sphere_t_inv(d3(s4.x, s4.y, s4.z), s4.w, r, T.a, T.inva, tmin, T.cl.c, t)) {
+            RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_hits;)
+            T.cl.lower(t);
+            T.found = true;
+            T.hit.t = t;
+            T.hit.ref = make_ref(K_SPHERE, sidx);
+        }
     }
     T.pn = pn;
     return T.cur != 0u || T.sp > 0 || pn > 0;
