@@ -623,7 +623,10 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     if ((rc = init_frame(cam, seed, p.row_offset, p.row_stride, f)) != RT_OK) return fail(rc);
     p.rows = f.rows;
     // The stratum rows of the frame's last RT_TAIL_PERMILLE / 1000 image rows
-    // (half) go out in parts of about RT_PART_SAMPLES (4) samples, every other
+    // (half; the mesh tier 0.65: C4 frame -0.5 % and worst 1/8 shard -2.3 %
+    // against half, profiles/r05/tail_sweep_c4.jsonl -- for C2 and C3 a longer
+    // tail costs the one-GPU frame 0.2-0.4 %) go out in parts of about
+    // RT_PART_SAMPLES (4; the mesh tier 2) samples, every other
     // row as one queue entry (rtk_row_parts, rtk_tail_rows; decided on the
     // whole frame, so shards and device counts sum rows alike): a launch ends
     // on short queue entries, since each shard's tail rows are its last.
@@ -647,7 +650,7 @@ static void run_part(rt_scene* s, RenderState* r, int32_t world, int32_t lights,
     f.parts = rtk_row_parts(f.S, env_u32("RT_PART_SAMPLES", d->tier == rtk::TIER_MESH ? 2 : 4));
     f.parts2 = rtk_row_parts(f.S, env_u32("RT_FINE_SAMPLES", 1));
     uint32_t tail = 0, fine = 0;
-    rtk_tail_split(f.W, H, f.S, f.parts, f.parts2, budget, env_u32("RT_TAIL_PERMILLE", 500),
+    rtk_tail_split(f.W, H, f.S, f.parts, f.parts2, budget, env_u32("RT_TAIL_PERMILLE", d->tier == rtk::TIER_MESH ? 650 : 500),
                    env_u32("RT_FINE_PERMILLE", 30), &tail, &fine);
     if (tail == 0) f.parts = 1;
     if (fine == 0) f.parts2 = f.parts;
