@@ -16,7 +16,14 @@ ranks split it.  value = traced samples of all steps / max-over-ranks time.
   python bench.py --workload c4        # BASELINE configs[3]: 1M-triangle OBJ, 1920x1080, 256 spp
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
-  python bench.py --gpus N --in-process
+  python bench.py --gpus N              # N > 1 without a launcher: in-process over devices 0..N-1
+
+Mode (select_mode): under torch.distributed.run (WORLD_SIZE > 1) one process
+per GPU, the library's RCCL communicator gathering to rank 0; with --gpus N >
+1 and no launcher (or --in-process), one process drives devices 0..N-1
+through rt_render_opts.devices -- ncclCommInitAll communicators and one
+ncclSend / ncclRecv group onto device 0.  The line names the gather the
+library used (rt_render_gather_mode) and its device time.
 """
 import argparse
 import ctypes
@@ -83,6 +90,43 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def select_mode(world_size, gpus, in_process):
+    """How bench.py runs --gpus N: "single" (one GPU, or this rank's rows of a
+    gloo rehearsal), "ranks" (torch.distributed.run, one process per GPU) or
+    "in-process" (one process, rt_render_opts.devices).  A plain
+    `python bench.py --gpus N` (N > 1, no launcher) is in-process, so the
+    multi-GPU line never depends on how the driver starts the script.
+    Raises ValueError for a launcher whose world size is not --gpus."""
+    if world_size > 1:
+        if in_process:
+            raise ValueError("--in-process runs as one process, not under torch.distributed.run")
+        if world_size != gpus:
+            raise ValueError(f"WORLD_SIZE {world_size} but --gpus {gpus}")
+        return "ranks"
+    if gpus > 1 or in_process:
+        return "in-process"
+    return "single"
+
+
+def parse_devices(text, gpus, device_count):
+    """The in-process device list: --devices "0,0,..." (a test may repeat a
+    device; the check build sends such a list through its RCCL stand-in),
+    else 0..gpus-1.  Raises ValueError when it does not fit the host."""
+    if text:
+        devs = [int(x) for x in text.split(",") if x.strip() != ""]
+        if len(devs) != gpus:
+            raise ValueError(f"--devices names {len(devs)} devices, --gpus is {gpus}")
+    else:
+        devs = list(range(gpus))
+    bad = [d for d in devs if d < 0 or d >= device_count]
+    if bad:
+        raise ValueError(f"--gpus {gpus} needs devices {devs}, this host has {device_count}")
+    return devs
+
+
+GATHER_MODES = {0: "none", 1: "rccl-communicator", 2: "rccl-device-list", 3: "peer-copy"}
 
 
 WORKLOADS = {  # BASELINE.json configs[1..4]: default width, spp
@@ -361,6 +405,12 @@ def main():
                          "gloo: rehearse ranks on one GPU with a torch gather (harness only)")
     ap.add_argument("--in-process", action="store_true",
                     help="one process drives --gpus N devices through rt_render_opts.devices (no torchrun)")
+    # test hooks (tests/test_bench_gpu.py): a repeated device list, the
+    # bounds-checked build (with RT_RCCL_LIB / RT_CHECK_RCCL_DUPS: the RCCL
+    # stand-in), the frame's hash in the line
+    ap.add_argument("--devices", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--lib", choices=("product", "check"), default="product", help=argparse.SUPPRESS)
+    ap.add_argument("--frame-hash", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this job may use")
     ap.add_argument("--cpu-row-stride", type=int, default=2)
     ap.add_argument("--cpu-spp", type=int, default=None, help="default: 64 (c2), 36 (c4) -> ~10 s of oracle work")
@@ -370,20 +420,21 @@ def main():
     if args.width is None:
         args.width = WORKLOADS[args.workload][0]
 
+    if args.lib == "check":  # before the package is imported: it reads RT_MI355X_LIB once
+        os.environ["RT_MI355X_LIB"] = os.path.join(ROOT, PKG, "librt_mi355x_check.so")
     import torch
     import torch.distributed as dist
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus and not args.in_process:
-        if world_size == 1 and args.gpus > 1:
-            print("bench.py: --gpus N > 1 must be launched with torch.distributed.run (one process per GPU), "
-                  "or with --in-process", file=sys.stderr)
-            sys.exit(2)
-    if args.in_process and world_size != 1:
-        print("bench.py: --in-process runs as one process", file=sys.stderr)
+    try:
+        mode = select_mode(world_size, args.gpus, args.in_process)
+        devices = parse_devices(args.devices, args.gpus, torch.cuda.device_count()) if mode == "in-process" else None
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
         sys.exit(2)
+    in_process = mode == "in-process"
     distributed = world_size > 1
     local_dev = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(local_dev)
@@ -432,13 +483,8 @@ def main():
     if lib_gather:
         opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0, comm=comm)
         rows = H if rank == 0 else 0
-    elif args.in_process:
-        n_dev = args.gpus
-        if n_dev > torch.cuda.device_count():
-            print(f"bench.py: --in-process --gpus {n_dev} but only {torch.cuda.device_count()} devices", file=sys.stderr)
-            sys.exit(2)
-        opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0,
-                                     devices=list(range(n_dev)))
+    elif in_process:
+        opts, keep = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0, devices=devices)
         rows = H
     else:
         # N = 1, or the gloo rehearsal: this rank renders its interleaved rows itself
@@ -494,7 +540,7 @@ def main():
         wc_path = os.path.join(ROOT, "bench_data", f"work_counts_{args.workload}.json")
         wc = json.load(open(wc_path))
         # one launch of the path kernel processes this rank's (or device's) rows
-        parts = max(world_size, args.gpus if args.in_process else 1)
+        parts = max(world_size, args.gpus if in_process else 1)
         launch_rows = -(-H // parts)
         launch_samples = W * launch_rows * sqrt_spp * sqrt_spp
         flops = wc["flops_per_sample"] * launch_samples
@@ -502,12 +548,13 @@ def main():
         tps, traffic_src = load_profile_field(f"pmc_{args.workload}.json", "hbm_bytes_per_sample")
         traffic = round(tps * launch_samples) if tps else None
         exec_fps, exec_src = load_profile_field(f"valu_{args.workload}.json", "executed_f64_flops_per_sample")
-        n = world_size if distributed else (args.gpus if args.in_process else 1)
+        n = world_size if distributed else (args.gpus if in_process else 1)
+        gmode = GATHER_MODES.get(api.render_gather_mode(scene.s), "?") if (lib_gather or in_process) else None
         how = ("one frame per step on one GPU" if n == 1 else
                f"one frame per step, rows interleaved over {n} GPUs, " +
                ("RCCL gather to rank 0 inside librt_mi355x.so (rt_comm_init)" if lib_gather else
-                "RCCL gather onto device 0 inside librt_mi355x.so (rt_render_opts.devices)" if args.in_process else
-                "torch gather to rank 0 (" + (gather_note or "gloo rehearsal harness") + ")"))
+                f"gather onto device {devices[0]} inside librt_mi355x.so (rt_render_opts.devices {devices}: {gmode})"
+                if in_process else "torch gather to rank 0 (" + (gather_note or "gloo rehearsal harness") + ")"))
         line = {
             "metric": {"c2": "Msamples/s (pixels x traced spp / s), book-1 random spheres 1920x1080, 512 spp (484 traced)",
                        "c3": "Msamples/s (pixels x traced spp / s), book-2 Cornell box + smoke 800x800, 1024 spp",
@@ -567,8 +614,15 @@ def main():
             line["roofline"]["executed_source"] = exec_src + " (rocprofv3 SQ_INSTS_VALU_*_F64 x 64 lanes x exec " \
                                                              "density, per traced sample) x this launch's samples"
         if n > 1:
+            line["gather"] = gmode or ("torch-" + args.backend)
             line["gather_ms_avg"] = round(sum(gather_ms) / len(gather_ms), 3)
-        if world_size == 1 and not args.in_process and not args.no_host_rate:
+            line["launch"] = mode
+        if args.lib != "product":
+            line["lib"] = os.path.basename(os.environ["RT_MI355X_LIB"])
+        if args.frame_hash:
+            import hashlib
+            line["frame_sha256"] = hashlib.sha256(frame[:H].contiguous().cpu().numpy().tobytes()).hexdigest()
+        if world_size == 1 and not in_process and not args.no_host_rate:
             # the PCIe-inclusive rate: rt_render into caller-owned host buffers
             # (linear f32 + sRGB bytes), SURVEY §8(d)'s t_render
             hopts, _hk = rt.Camera._opts(api, args.seed, 0, 1, 0, 1 if args.reference_bvh else 0)
@@ -585,7 +639,7 @@ def main():
                                       "ms": round(dh * 1e3, 3), "kernel_ms": round(hst.kernel_ms, 3),
                                       "note": "one rt_render into host buffers (linear f32 + sRGB u8, PCIe copy "
                                               "included), after the timed steps; not `value`"}
-        if world_size == 1 and not args.in_process and not args.no_cpu_baseline:
+        if world_size == 1 and not in_process and not args.no_cpu_baseline:
             cpu_spp = args.cpu_spp or {"c2": 64, "c3": 400, "c4": 36, "c5": 16}[args.workload]
             threads, info = usable_cpus()
             if args.cpu_threads:

@@ -251,6 +251,19 @@ int32_t rt_render_device(rt_scene* s, int32_t world, int32_t lights, const rt_ca
 /* Waits for the last rt_render_device on this scene and reports its stats
  * (an earlier call's stats are superseded by a later call's). */
 int32_t rt_render_device_wait(rt_scene* s, rt_stats* stats);
+/* How the last render on this scene brought its parts to devices[0] / rank 0
+ * (the transfer rt_stats.gather_ms times; the replacement of rayon's join of
+ * the pixel iterator, camera.rs:178-197): RT_GATHER_NONE (one part, nothing
+ * gathered), RT_GATHER_RCCL_COMM (one ncclSend / ncclRecv group over an
+ * rt_comm_init communicator), RT_GATHER_RCCL_DEVICES (one group over the
+ * ncclCommInitAll communicators of a device list), RT_GATHER_PEER_COPY
+ * (hipMemcpyPeerAsync: a device listed twice, or librccl absent); < 0 when
+ * nothing was rendered on the scene. */
+#define RT_GATHER_NONE 0
+#define RT_GATHER_RCCL_COMM 1
+#define RT_GATHER_RCCL_DEVICES 2
+#define RT_GATHER_PEER_COPY 3
+int32_t rt_render_gather_mode(const rt_scene* s);
 
 /* Test hook (parity tooling, not part of the reference surface): the f64 sum
  * of each (pixel, stratum row s_i) of the last single-device render on this

@@ -121,6 +121,7 @@ SIGNATURES = {
     "shard_rows": (_U, [C.POINTER(RtCamera), C.POINTER(RtRenderOpts)]),
     "render_device": (_I, [_P, _I, _I, C.POINTER(RtCamera), C.POINTER(RtRenderOpts), _P]),
     "render_device_wait": (_I, [_P, C.POINTER(RtStats)]),
+    "render_gather_mode": (_I, [_P]),
     "to_rgb_device": (_I, [_P, _P, C.c_uint64, _I, _P]),
     "write_png": (_I, [C.c_char_p, C.c_uint32, C.c_uint32, _P]),
     "camera_from_json": (_I, [C.c_char_p, C.POINTER(RtCamera)]),
@@ -136,7 +137,7 @@ SIGNATURES = {
 
 # Entry points of the product library only (the oracle renders on host cores
 # and has no communicator, device-side partial sums or parallel builders).
-GPU_ONLY = ("render_partials_get", "math_selftest", "bvh_selftest", "world_selftest", "comm_unique_id", "comm_init", "comm_destroy")
+GPU_ONLY = ("render_gather_mode", "render_partials_get", "math_selftest", "bvh_selftest", "world_selftest", "comm_unique_id", "comm_init", "comm_destroy")
 
 # Entry points only a CPU implementation has (the oracle).
 ORACLE_EXTRAS = {

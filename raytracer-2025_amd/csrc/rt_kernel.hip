@@ -1883,15 +1883,18 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             // measured +0.4 % on C4 with it and keeps unit())
             // Basic tier under a sky gradient (the world's background
             // is wave-uniform: a scalar branch): the gradient reads the unit
-            // direction's y only, so only that quotient is made.  `ok` is the
-            // same as unit()'s finite3 of the three quotients: with l =
-            // |d| not NaN and not 0 and every component finite, each d_i / l
-            // is finite (|d_i| <= l, or l = inf over finite components: 0);
-            // l = 0 or NaN, or an infinite component (inf / inf), gives a NaN
+            // direction's y only, so only that component is made, as unit()
+            // makes it: (1 / l) * d.y (vec3.rs:225-232, rt_math.h divs).
+            // `ok` is the same as unit()'s finite3 of the three products:
+            // with l = |d| not NaN and not 0 and every component finite,
+            // 1 / l is finite (a nonzero l is >= sqrt(5e-324) ~ 2e-162) and
+            // each (1 / l) * d_i is finite (|d_i| <= l, or l = inf over
+            // finite components: 0); l = 0 or NaN, or an infinite component
+            // (0 * inf), gives a NaN (tests/test_miss_unit_cpu.py)
             if (S.background_tex >= 0 && S.textures[S.background_tex].type == T_SKY) {
                 const double l = len(ray.d);
                 if (isnan(l) || l == 0.0 || !finite3(ray.d)) panic = true;
-                L = L + beta * sky_value(S.textures[S.background_tex], ray.d.y / l);
+                L = L + beta * sky_value(S.textures[S.background_tex], (1.0 / l) * ray.d.y);
                 return true;
             }
         }
@@ -2283,7 +2286,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     uint32_t slot = 0, s_j = 0, sie = 0;
     bool need = true;
     bool in_path = false;
-    Ray ray;
+    // defined from the start: the basic tier's walk-field set-up reads it for
+    // lanes without a path too (values never used; no indeterminate read)
+    Ray ray{};
     D3 beta = d3(1, 1, 1), L = d3(0, 0, 0), acc = d3(0, 0, 0);
     uint32_t vertex = 0;
     uint32_t n_rays = 0, n_panics = 0;
@@ -2853,14 +2858,15 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         atomicAdd(&g_diag[28 + k], dg.l_top[k]);
     }
     atomicAdd(&g_diag[32], dg.l_node);
-    if (lane == 0) {
-        atomicAdd(&g_diag[33], dg.sh_rounds);
-        atomicAdd(&g_diag[34], dg.sh_lanes);
-        atomicAdd(&g_diag[35], dg.sh_classes);
-        atomicAdd(&g_diag[36], dg.pure_rounds);
-        atomicAdd(&g_diag[37], dg.pure_lanes);
-        atomicAdd(&g_diag[38], dg.pure_max_pn);
-    }
+    // counted by the first active lane of a round, which need not be lane 0
+    // (lanes whose walk has ended are masked off): flushed from every lane,
+    // as g_diag[3]
+    atomicAdd(&g_diag[33], dg.sh_rounds);
+    atomicAdd(&g_diag[34], dg.sh_lanes);
+    atomicAdd(&g_diag[35], dg.sh_classes);
+    atomicAdd(&g_diag[36], dg.pure_rounds);
+    atomicAdd(&g_diag[37], dg.pure_lanes);
+    atomicAdd(&g_diag[38], dg.pure_max_pn);
 #endif
 #ifdef RT_WAVE_TRACE
     hist.flush();

@@ -176,6 +176,7 @@ struct RenderState {
     // the last render
     int n_parts = 0;
     bool gathered = false;
+    int gather_mode = RT_GATHER_NONE;  // rt_render_gather_mode
     bool pending = false;
     bool is_root = true;
     hipStream_t root_stream = nullptr;
@@ -852,6 +853,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         r->n_parts = 0;
         r->pending = false;
         r->gathered = false;
+        r->gather_mode = RT_GATHER_NONE;
         return set_error(code, msg);
     };
     double flatten_ms = 0;
@@ -864,6 +866,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
     }
     r->n_parts = (int)parts.size();
     r->gathered = gather;
+    r->gather_mode = RT_GATHER_NONE;
     r->is_root = is_root;
     r->flatten_ms = flatten_ms;
     r->root_stream = parts[0].stream;
@@ -896,6 +899,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
 #endif
         if (comm) {
             if (!nc.ok) return abort_render(set_error(RT_EDEVICE, nc.err));
+            r->gather_mode = RT_GATHER_RCCL_COMM;
             std::lock_guard<std::mutex> glk(comm->group);  // the whole group, enqueued at once
             ncclResult_t ne = nc.group_start();
             if (ne == ncclSuccess)
@@ -916,6 +920,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
             const std::vector<int> devs(opts->devices, opts->devices + nd);
             if ((rc = acquire_comms(r, nc, devs)) != RT_OK) return abort_render(rc);
             CommSet& cs = *r->comm_set;
+            r->gather_mode = RT_GATHER_RCCL_DEVICES;
             std::lock_guard<std::mutex> glk(cs.group);  // the whole group, enqueued at once
             ncclResult_t ne = nc.group_start();
             for (uint32_t k = 0; k < nd && ne == ncclSuccess; ++k) {
@@ -938,6 +943,7 @@ static int32_t launch(rt_scene* s, int32_t world, int32_t lights, const rt_camer
         } else {
             // a device listed twice (one communicator per device is all RCCL
             // allows) or no librccl: peer copies onto the root
+            r->gather_mode = RT_GATHER_PEER_COPY;
             for (uint32_t k = 0; k < nd; ++k) {
                 if (!parts[k].rows) continue;
                 if ((e = hipStreamWaitEvent(rs, parts[k].d->ev_done, 0)) != hipSuccess)
@@ -1077,6 +1083,12 @@ int32_t rt_world_info_get(rt_scene* s, int32_t world, int32_t lights, int32_t bg
 
 int32_t rt_render_device_wait(rt_scene* s, rt_stats* st) {
     return wait(s, st);
+}
+
+int32_t rt_render_gather_mode(const rt_scene* s) {
+    const RenderState* r = s ? s->rs : nullptr;
+    if (!r || r->n_parts == 0) return set_error(RT_EINVAL, "nothing rendered on this scene");
+    return r->gather_mode;
 }
 
 int32_t rt_render_partials_get(rt_scene* s, double* out, uint64_t n_values) {

@@ -98,7 +98,9 @@ def main(workload="c2", row_stride=None, spp=None, threads=0):
         "weights_flops": WEIGHTS,
         "flops_per_sample": flops,
         "cache_bytes_per_sample": bytes_,
-        "hbm_bytes_per_pixel": 24 * cam.sqrt_spp + 12,
+        # at the CONFIG's strata, not the sampled run's: one 24-B part sum per
+        # stratum row of the pixel (rt_path_kernel) + its 12-B f32 output
+        "hbm_bytes_per_pixel": hbm_bytes_per_pixel(workload),
         "cpu_seconds": st.render_ms / 1e3,
     }
     path = os.path.join(ROOT, "bench_data", "work_counts_%s.json" % workload)
@@ -106,6 +108,16 @@ def main(workload="c2", row_stride=None, spp=None, threads=0):
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
+
+
+# sqrt_spp of each BASELINE config (512 -> 22, 1024 -> 32, 256 -> 16, 4096 -> 64)
+CONFIG_SQRT_SPP = {"c2": 22, "c3": 32, "c4": 16, "c5": 64}
+
+
+def hbm_bytes_per_pixel(workload):
+    """Algorithmic HBM bytes per pixel of a config's frame: the path kernel's
+    part sums (3 f64 per stratum row) and the reduce's f32 pixel."""
+    return 24 * CONFIG_SQRT_SPP[workload] + 12
 
 
 if __name__ == "__main__":

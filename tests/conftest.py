@@ -75,6 +75,27 @@ def gpu(product):
     return product
 
 
+@pytest.fixture(scope="session")
+def rccl_standin(tmp_path_factory):
+    """The test-only RCCL stand-in (tests/cpp/fake_rccl.cpp: librccl's
+    point-to-point subset over hipMemcpyPeerAsync, any number of ranks per
+    device), built for this run (host code, g++ against the HIP runtime).
+    Returns (path of the .so, counts()) -- counts() = (copies, bytes) so far
+    in this process.  Only the check build loads it (RT_RCCL_LIB)."""
+    src = os.path.join(ROOT, "tests", "cpp", "fake_rccl.cpp")
+    so = str(tmp_path_factory.mktemp("standin") / "libfake_rccl.so")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    src, "-o", so, "-L/opt/rocm/lib", "-lamdhip64", "-pthread"], check=True, timeout=120)
+    lib = ctypes.CDLL(so)
+    lib.fake_rccl_counts.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+
+    def counts():
+        out = (ctypes.c_uint64 * 2)()
+        lib.fake_rccl_counts(out)
+        return int(out[0]), int(out[1])
+    return so, counts
+
+
 def rmse_per_channel(a, b):
     import numpy as np
 

@@ -75,3 +75,55 @@ def test_bench_two_ranks_gloo():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["frame_samples"] == 256 * 144 * 16 and d["value"] > 0
+
+
+def _bench_env(**extra):
+    env = dict(os.environ)
+    env.update(extra)
+    return env
+
+
+def test_bench_multi_gpu_without_launcher_standin(rccl_standin):
+    """`python bench.py --gpus 8`, the shape of the driver's bench command
+    with no torch.distributed.run, renders in-process over a device list
+    (rt_render_opts.devices -> ncclCommInitAll -> one send / receive group).
+    On the one-GPU box the list is device 0 eight times, through the check
+    build and the RCCL stand-in (RT_CHECK_RCCL_DUPS=1 sends a repeated list
+    through the RCCL group): one JSON line, n_gpus 8, the RCCL device-list
+    gather, and a frame hash equal to the one-GPU frame's."""
+    so, _ = rccl_standin
+    common = ["--steps", "2", "--warmup", "1", "--width", "256", "--spp", "16", "--no-cpu-baseline",
+              "--no-host-rate", "--lib", "check", "--frame-hash"]
+    env = _bench_env(RT_RCCL_LIB=so, RT_CHECK_RCCL_DUPS="1")
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *common],
+                        capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][0])
+    r8 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8",
+                         "--devices", ",".join(["0"] * 8), *common],
+                        capture_output=True, text=True, timeout=110, cwd=ROOT, env=env)
+    assert r8.returncode == 0, r8.stderr[-3000:]
+    lines = [l for l in r8.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r8.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["launch"] == "in-process" and d["gather"] == "rccl-device-list"
+    assert d["lib"] == "librt_mi355x_check.so" and one["lib"] == "librt_mi355x_check.so"
+    assert d["gather_ms_avg"] > 0 and d["config"]["frame_samples"] == 256 * 144 * 16
+    assert d["frame_sha256"] == one["frame_sha256"]
+
+
+def test_bench_repeated_devices_peer_copy():
+    """The product library with a repeated device list (real RCCL refuses two
+    ranks on one device): the parts reach device 0 by peer copies, named in the
+    line, and the frame is the one-GPU frame."""
+    common = ["--steps", "1", "--warmup", "1", "--width", "128", "--spp", "4", "--no-cpu-baseline",
+              "--no-host-rate", "--frame-hash"]
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", *common],
+                        capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads([l for l in r1.stdout.splitlines() if l.startswith("{")][0])
+    r3 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--devices", "0,0,0",
+                         *common], capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert r3.returncode == 0, r3.stderr[-3000:]
+    d = json.loads([l for l in r3.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 3 and d["gather"] == "peer-copy" and d["frame_sha256"] == one["frame_sha256"]

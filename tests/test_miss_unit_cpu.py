@@ -12,14 +12,24 @@ def _len(v):
     return np.sqrt(v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1] + v[:, 2] * v[:, 2])
 
 
-def _ok_unit(v):  # unit(): every quotient finite
+def _ok_unit(v):  # unit() = divs(v, |v|) = (1 / |v|) * v (rt_math.h, vec3.rs:225-232): every product finite
     l = _len(v)
-    return np.isfinite(v / l[:, None]).all(axis=1), (v[:, 1] / l)
+    u = (1.0 / l)[:, None] * v
+    return np.isfinite(u).all(axis=1), u[:, 1]
 
 
-def _ok_sky(v):  # the kernel's statement
+def _ok_sky(v):  # the kernel's statement (rt_kernel.hip shade, basic tier's sky miss)
     l = _len(v)
-    return ~(np.isnan(l) | (l == 0.0) | ~np.isfinite(v).all(axis=1)), (v[:, 1] / l)
+    return ~(np.isnan(l) | (l == 0.0) | ~np.isfinite(v).all(axis=1)), ((1.0 / l) * v[:, 1])
+
+
+def test_division_form_differs_from_reciprocal_form():
+    """d.y / l is not (1 / l) * d.y: the y the gradient reads must be made the
+    reference's way, and this shows the check can tell them apart."""
+    rng = np.random.default_rng(7)
+    v = rng.standard_normal((20000, 3))
+    l = _len(v)
+    assert ((v[:, 1] / l) != ((1.0 / l) * v[:, 1])).mean() > 0.05
 
 
 def _cases():
