@@ -24,6 +24,7 @@
 #include "rt_math.h"
 #include "rt_slab.h"
 #include "rt_sphere_filter.h"
+#include "rt_plan.h"
 
 namespace rtk {
 
@@ -3173,16 +3174,7 @@ __global__ void __launch_bounds__(256) rt_deinterleave_u8_kernel(const uint8_t* 
 }  // namespace rtk
 
 extern "C" int rtk_tier_for(uint32_t features, uint32_t stack_need) {
-    const uint32_t full = rtk::F_XFORM | rtk::F_MEDIUM | rtk::F_MSPHERE | rtk::F_LIGHTS | rtk::F_TEXFULL | rtk::F_MATFULL |
-                          rtk::F_NORMALMAP;
-    if (features & rtk::F_GENERAL) return rtk::TIER_FULL_GL;
-    if (features & full) return rtk::TIER_FULL;
-    if (features & (rtk::F_PLANAR | rtk::F_REMAP)) return rtk::TIER_MESH;
-    // the two-box tree's stack need; with 4-wide nodes the launcher decides on
-    // the 4-wide tree's (shallower: a 1 500-sphere world needs 22 entries as
-    // two-box nodes and fits the basic tier's 14 as 4-wide ones)
-    if (!RT_BVH4 && stack_need > RT_STACK_BASIC) return rtk::TIER_MESH;
-    return rtk::TIER_BASIC;
+    return rtk::plan::tier_for(features, stack_need, RT_BVH4 != 0, RT_STACK_BASIC);
 }
 
 extern "C" int rtk_basic_bvh4(void) { return RT_BVH4; }
@@ -3340,65 +3332,23 @@ extern "C" hipError_t rtk_launch_to_rgb(const float* lin, uint8_t* srgb, uint64_
     return hipGetLastError();
 }
 
-extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples) {
-    if (part_samples == 0 || S <= part_samples) return 1;
-    const uint32_t parts = (S + part_samples - 1) / part_samples;
-    const uint32_t len = (S + parts - 1) / parts;
-    return (S + len - 1) / len;  // as many parts of that length as S takes: none empty
-}
+// the frame plan (rt_plan.h), for rt_render.cpp
+extern "C" uint32_t rtk_row_parts(uint32_t S, uint32_t part_samples) { return rtk::plan::row_parts(S, part_samples); }
 
 extern "C" uint32_t rtk_tail_rows(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint64_t budget_bytes,
                                   uint32_t permille) {
-    if (parts <= 1 || W == 0 || S == 0) return 0;
-    uint64_t t = ((uint64_t)H * permille + 999) / 1000;
-    if (t > H) t = H;
-    // the tail's part sums beyond one sum per row within the budget
-    const uint64_t extra_row = (uint64_t)W * S * (parts - 1);
-    const uint64_t by_budget = budget_bytes / (extra_row * 3 * sizeof(double));
-    if (t > by_budget) t = by_budget;
-    // the queue of the whole frame below 2^32 entries
-    const uint64_t whole = (uint64_t)W * H * S;
-    if (whole >= 0xFFF00000ull) return 0;
-    const uint64_t by_queue = (0xFFF00000ull - 1 - whole) / extra_row;
-    if (t > by_queue) t = by_queue;
-    return (uint32_t)t;
+    return rtk::plan::tail_rows(W, H, S, parts, budget_bytes, permille);
 }
 
 extern "C" void rtk_tail_split(uint32_t W, uint32_t H, uint32_t S, uint32_t parts, uint32_t parts2,
                                uint64_t budget_bytes, uint32_t permille, uint32_t fine_permille, uint32_t* tail,
                                uint32_t* fine) {
-    *tail = *fine = 0;
-    if (parts <= 1 || W == 0 || S == 0) return;
-    const uint64_t whole = (uint64_t)W * H * S;
-    if (whole >= 0xFFF00000ull) return;
-    uint64_t room = 0xFFF00000ull - 1 - whole;  // queue entries beyond one per stratum row
-    uint64_t f = 0;
-    if (parts2 > parts) {
-        f = ((uint64_t)H * fine_permille + 999) / 1000;
-        if (f > H) f = H;
-        const uint64_t extra_f = (uint64_t)W * S * (parts2 - 1);
-        f = std::min<uint64_t>(f, (budget_bytes / 2) / (extra_f * 3 * sizeof(double)));
-        f = std::min<uint64_t>(f, (room / 2) / extra_f);
-        budget_bytes -= f * extra_f * 3 * sizeof(double);
-        room -= f * extra_f;
-    }
-    uint64_t tp = ((uint64_t)H * permille + 999) / 1000;  // the whole tail, fine rows included
-    if (tp > H) tp = H;
-    tp = tp > f ? tp - f : 0;  // its rows in `parts`
-    const uint64_t extra_row = (uint64_t)W * S * (parts - 1);
-    tp = std::min<uint64_t>(tp, budget_bytes / (extra_row * 3 * sizeof(double)));
-    tp = std::min<uint64_t>(tp, room / extra_row);
-    *fine = (uint32_t)f;
-    *tail = (uint32_t)(f + tp);
+    rtk::plan::tail_split(W, H, S, parts, parts2, budget_bytes, permille, fine_permille, tail, fine);
 }
 
 extern "C" uint32_t rtk_shard_whole_rows(uint32_t H, uint32_t tail, uint32_t row_offset, uint32_t row_stride,
                                          uint32_t rows) {
-    const uint32_t whole_img = tail < H ? H - tail : 0u;
-    const uint32_t stride = row_stride ? row_stride : 1u;
-    if (whole_img <= row_offset) return 0u;
-    const uint32_t n = (whole_img - row_offset + stride - 1) / stride;
-    return n < rows ? n : rows;
+    return rtk::plan::shard_whole_rows(H, tail, row_offset, row_stride, rows);
 }
 
 extern "C" size_t rtk_params_bytes(void) { return sizeof(rtk::KParams); }
