@@ -83,6 +83,14 @@ __device__ unsigned long long g_diag[RT_DIAG_N];
 #else
 #define RT_DIAG_ONLY(x)
 #endif
+// ISA attribution build only (scripts/isa_phases.py, -DRT_ISA_MARKS): an
+// assembler comment at each phase boundary of the basic tier's loop, so that
+// the static instruction mix of every phase can be read off the ISA
+#ifdef RT_ISA_MARKS
+#define RT_ISA_MARK(name) asm volatile(";@@phase " name)
+#else
+#define RT_ISA_MARK(name)
+#endif
 
 #ifdef RT_WAVE_TRACE
 // trace build: per lane of the grid, {start, end (s_memrealtime, 100 MHz),
@@ -275,11 +283,18 @@ __device__ __forceinline__ double tex_alpha(const SceneView& S, int tid, double 
     return (double)px[3];
 }
 
+#ifndef RT_BG_PARAMS
+// 1: the basic and mesh tiers' miss under a sky gradient reads its colours
+// from the launch parameters (SceneView::bg_c0 / bg_c1); 0: from the texture
+// table (A/B only)
+#define RT_BG_PARAMS 1
+#endif
 // the sky gradient (rt_tex_sky_gradient, include/rt_mi355x.h) at the unit direction's y
-__device__ __forceinline__ D3 sky_value(const DTexture& t, double py) {
+__device__ __forceinline__ D3 sky_value(const double* c0, const double* c1, double py) {
     const double a = 0.5 * (py + 1.0);
-    return (1.0 - a) * d3(t.color[0], t.color[1], t.color[2]) + a * d3(t.color2[0], t.color2[1], t.color2[2]);
+    return (1.0 - a) * d3(c0[0], c0[1], c0[2]) + a * d3(c1[0], c1[1], c1[2]);
 }
+__device__ __forceinline__ D3 sky_value(const DTexture& t, double py) { return sky_value(t.color, t.color2, py); }
 
 template <bool FULL, bool PL = false>  // PL: NoiseTexture reads the LDS copy of the first Perlin table
 __device__ D3 tex_value(const SceneView& S, int tid, double u, double v, D3 p) {
@@ -1500,6 +1515,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
         }
     }
     if (node) {
+        RT_ISA_MARK("walk_visit");
         RT_DIAG_ONLY(++dg.node_visits;)
         T.cur = visit4_rows(S, rows, T.rf, T.sf, tmin_f, T.cl.c_f, stk, T.sp, pq, pn);
     }
@@ -1509,6 +1525,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
     // visit culls against the closest t before this test, which only makes
     // it cull less, never wrongly)
     if (round) {  // sphere round (sphere.rs:77-108)
+        RT_ISA_MARK("walk_sphere");
         RT_DIAG_ONLY(++dg.sphere_tests;)
         double t;
         RT_DIAG_ONLY(if (s4.w > 100.0) ++dg.big_tests;)
@@ -1520,6 +1537,7 @@ __device__ __forceinline__ bool trace4_step(const SceneView& S, const Ray& r, Tr
             T.hit.ref = make_ref(K_SPHERE, sidx);
         }
     }
+    RT_ISA_MARK("walk_tail");
     T.pn = pn;
     return T.cur != 0u || T.sp > 0 || pn > 0;
 }
@@ -1892,12 +1910,23 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             // each (1 / l) * d_i is finite (|d_i| <= l, or l = inf over
             // finite components: 0); l = 0 or NaN, or an infinite component
             // (0 * inf), gives a NaN (tests/test_miss_unit_cpu.py)
-            if (S.background_tex >= 0 && S.textures[S.background_tex].type == T_SKY) {
+            // The gradient's colours come with the launch parameters
+            // (SceneView::bg_c0 / bg_c1), not from the texture table.
+            if (RT_BG_PARAMS ? S.bg_kind == BG_SKY
+                             : (S.background_tex >= 0 && S.textures[S.background_tex].type == T_SKY)) {
                 const double l = len(ray.d);
                 if (isnan(l) || l == 0.0 || !finite3(ray.d)) panic = true;
-                L = L + beta * sky_value(S.textures[S.background_tex], (1.0 / l) * ray.d.y);
+                L = L + beta * (RT_BG_PARAMS ? sky_value(S.bg_c0, S.bg_c1, (1.0 / l) * ray.d.y)
+                                             : sky_value(S.textures[S.background_tex], (1.0 / l) * ray.d.y));
                 return true;
             }
+        }
+        if (RT_BG_PARAMS && !FULL && S.bg_kind == BG_SKY) {  // the mesh tier: unit(), the gradient from the launch parameters
+            bool ok;
+            const D3 p = unit(ray.d, ok);
+            if (!ok) panic = true;
+            L = L + beta * sky_value(S.bg_c0, S.bg_c1, p.y);
+            return true;
         }
         if (S.background_tex >= 0) {
             bool ok;
@@ -2087,6 +2116,128 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
         ray = Ray{rec.p, dir, ray.time};
     }
     if (ovf) panic = true;
+    return panic;
+}
+
+// ------------------------------------------------------------------ basic tier: one hit, merged
+#ifndef RT_SHADE_MERGED
+// 1: the basic tier shades a hit with shade_hit_basic (below), 0: with shade
+// (A/B only)
+#define RT_SHADE_MERGED 1
+#endif
+// shade() for a hit in the basic tier (camera.rs:286-316; Lambertian /
+// EmptyMaterial, Metal, Dielectric: material.rs:41-143, onb.rs:8-38,
+// pdf.rs:50-63), with the three scatter codes' square roots and divisions
+// merged.  As one switch, a wave whose shading batch holds all three
+// classes ran every class's unit vectors, square roots and divisions one
+// after the other (10 square roots and 9 divisions); here each stage is one
+// square root or division that every lane runs on its own class's operand:
+//   A  unit(cross(n, a)) (Lambertian's ONB)  |  unit(r_in.direction) (Metal, Dielectric)
+//   B1 sqrt(r2)  |  sqrt(r2 (1 - r2)) (random_unit_vector)  |  sin_theta
+//   B2 sqrt(1 - r2) (Lambertian)
+//   C  unit(direction) (Lambertian)  |  unit(reflect) (Metal);  1 / ior (Dielectric, front face)
+//   D1 cos_theta / PI (Lambertian pdf)  |  r0 = (1 - ri) / (1 + ri) (Dielectric, Schlick)
+//   D2 1 / pdf (Lambertian);  E  the refracted ray's sqrt (Dielectric)
+// Every lane computes exactly the operations of its class, in the
+// reference's order (the same doubles as shade()); only the instructions
+// are shared.  Returns true when the path ends (panic: a reference panic
+// condition).
+__device__ __forceinline__ bool shade_hit_basic(const SceneView& S, Ray& ray, D3& beta, const HitInfo& h, bool& panic,
+                                                const Draws& Dr) {
+    const Rec rec = make_record<TIER_BASIC>(S, ray, h, panic);
+    if (panic) return true;
+    const DMaterial M = S.materials[rec.mat];
+    constexpr int LAMB = 0, METAL = 1, DIEL = 2;
+    const int cls = (M.type == M_LAMBERTIAN || M.type == M_EMPTY) ? LAMB
+                  : M.type == M_METAL ? METAL : M.type == M_DIELECTRIC ? DIEL : 3;
+    if (cls == 3) return true;  // (no other material reaches the basic tier)
+    const D3 n = rec.n;
+    const double xi0 = Dr.xi0, xi1 = Dr.xi1, sn0 = Dr.sn, cs0 = Dr.cs;
+    // the albedo (Lambertian, material.rs:60-65) or attenuation (Dielectric, :141)
+    D3 tex = d3(0.75, 0.75, 0.75);  // EmptyMaterial (material.rs:41-46)
+    if (M.type == M_LAMBERTIAN || cls == DIEL) tex = mat_tex<false, false>(S, M, rec.u, rec.v, rec.p);
+    // ---- A
+    D3 vA = ray.d;
+    if (cls == LAMB) {  // onb.rs:8-21
+        const D3 a = fabs(n.x) > 0.9 ? d3(0.0, 1.0, 0.0) : d3(1.0, 0.0, 0.0);
+        vA = cross(n, a);
+    }
+    bool okA;
+    const D3 uA = unit(vA, okA);
+    if (!okA) {
+        if (cls == METAL) return true;  // material.rs:83: r_in.direction not normalizable -> None
+        panic = true;                   // onb.rs / material.rs:120: .expect
+    }
+    // ---- B1, B2
+    double cosd = 0.0, xB1 = xi1;  // Lambertian: r2 (vec3.rs:333-343)
+    if (cls == METAL) xB1 = xi1 * (1.0 - xi1);  // vec3.rs:313-322
+    if (cls == DIEL) {                          // material.rs:121-122
+        cosd = fmin(dot(-uA, n), 1.0);
+        xB1 = 1.0 - cosd * cosd;
+    }
+    const double sB1 = sqrt(xB1);
+    double sB2 = 0.0;
+    if (cls == LAMB) sB2 = sqrt(1.0 - xi1);
+    // ---- C
+    D3 vC = ray.d;
+    if (cls == LAMB) {  // onb_world: v.x u + v.y n + v.z w (onb.rs:34-38)
+        const D3 w = cross(uA, n);
+        const D3 v = d3(sn0 * sB1, sB2, cs0 * sB1);
+        vC = v.x * uA + v.y * n + v.z * w;
+    } else if (cls == METAL) {
+        vC = reflect(uA, n);
+    }
+    const double lC = len(vC);
+    const double qC = 1.0 / (cls == DIEL ? M.fuzz : lC);  // unit(): (1 / |v|) v; Dielectric: 1 / ior
+    const D3 uC = qC * vC;
+    const bool okC = finite3(uC);
+    if (cls == METAL) {  // material.rs:82-95
+        if (!okC) return true;
+        const double s = sB1;
+        const D3 ruv = d3(cs0 * 2.0 * s, sn0 * 2.0 * s, 1.0 - 2.0 * xi1);
+        beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
+        ray = Ray{rec.p, uC + (M.fuzz * ruv), ray.time};
+        return panic;
+    }
+    // ---- D1
+    double ct = 0.0, ri = 0.0;
+    bool refl = false;
+    if (cls == LAMB) {
+        if (!okC) panic = true;  // pdf.rs:22-28 (the direction's unit)
+        ct = dot(uC, n);
+    } else {  // Dielectric: ri (material.rs:118), total internal reflection (:123)
+        ri = rec.front ? qC : M.fuzz;
+        refl = ri * sB1 > 1.0;
+    }
+    const double qD1 = (cls == LAMB ? ct : 1.0 - ri) / (cls == LAMB ? PI : 1.0 + ri);
+    if (cls == LAMB) {  // pdf.rs:50-57, camera.rs:305-316
+        const double pdf = fmax(0.0, qD1);
+        const double cp = fmax(ct, 0.0);
+        const D3 f = divs(tex * d3(cp, cp, cp), PI);
+        if (pdf == 0.0) panic = true;  // camera.rs:309
+        beta = beta * divs(f, pdf);
+        ray = Ray{rec.p, vC, ray.time};
+        return panic;
+    }
+    // Dielectric: Schlick (material.rs:110-114), the draw only when refraction is possible
+    if (!refl) {
+        const double r0 = qD1;
+        const double r0sq = r0 * r0;
+        const double x = 1.0 - cosd;
+        const double x2 = x * x;
+        refl = r0sq + (1.0 - r0sq) * (x * (x2 * x2)) > xi0;
+    }
+    D3 dir;
+    if (refl) {
+        dir = reflect(uA, n);
+    } else {  // vec3.rs:345-354
+        const D3 perp = ri * (uA + cosd * n);
+        const double pl = sqrt(1.0 - len2(perp));
+        if (isnan(pl)) panic = true;
+        dir = perp + (-pl * n);
+    }
+    beta = beta * tex;
+    ray = Ray{rec.p, dir, ray.time};
     return panic;
 }
 
@@ -2407,10 +2558,12 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         acc = acc + L;
         ++s_j;
         if (s_j == (sie >> 16)) {
+#ifndef RT_MEASURE_NOSTORE
             double* dst = P->partial + (uint64_t)slot * 3;
             dst[0] = acc.x;
             dst[1] = acc.y;
             dst[2] = acc.z;
+#endif
             need = true;
         }
     };
@@ -2428,7 +2581,9 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             double xi0 = Dr.xi0, xi1 = Dr.xi1;
             D3 origin = F.center;
             if (F.defocus) {  // vec3.rs:63-69: theta = 2 pi Dr.xi0, r = sqrt(Dr.xi1)
+#ifndef RT_MEASURE_NOCAMPAIR
                 rng.pair(0u, 0u, xi0, xi1);
+#endif
                 const double rr = sqrt(Dr.xi1);
                 origin = (F.center + ((rr * Dr.cs) * F.disk_u)) + ((rr * Dr.sn) * F.disk_v);
             }
@@ -2445,6 +2600,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         };
         for (;;) {
             RT_DIAG_ONLY(const unsigned long long t_loop0 = __builtin_amdgcn_s_memtime(); ++dg.main_iters;)
+            RT_ISA_MARK("fields");
 #ifdef RT_WAVE_TRACE
             hist.add(__ballot(!no_path && !walking));
 #endif
@@ -2485,6 +2641,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 walking = true;
             }
             RT_DIAG_ONLY(const unsigned long long t_b0 = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_b0 - t_loop0;)
+            RT_ISA_MARK("walk");
             auto step = [&]() -> bool {
                 if constexpr (TIER == TIER_BASIC && RT_BVH4) {
                     return trace4_step(S, ray, T, stk, pq, (const RT_LDS float4*)node_lds, dg);
@@ -2513,6 +2670,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             // which every lane of the wave runs: the queue pool (pool_next,
             // pool_end, dry) is wave-uniform state and must be updated in
             // uniform control flow, or a parked lane would keep a stale copy
+            RT_ISA_MARK("park");
             const bool carry = BATCH < 64 && walking;
             if constexpr (PARK) {
                 if (carry) trace_park2(T, pk2);
@@ -2520,19 +2678,24 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             // ---- this lane's walk is over, or it has no path
             bool cam = no_path;
             if (!carry && !no_path && !T.found) {  // a miss: Environment::value, and the sample ends
+                RT_ISA_MARK("miss");
+#ifndef RT_MEASURE_NOSKY
                 bool panic = false;
                 shade<TIER>(S, ray, beta, L, rng, false, T.hit, panic);
                 if (panic) ++n_panics;
+#endif
                 finish_sample();
                 cam = true;
             }
             RT_DIAG_ONLY(const unsigned long long t_m = __builtin_amdgcn_s_memtime(); dg.cyc_miss += t_m - t_b1;)
+            RT_ISA_MARK("refill");
             if (!refill()) break;
             RT_DIAG_ONLY(const unsigned long long t_q = __builtin_amdgcn_s_memtime(); dg.cyc_queue += t_q - t_m;)
             if (carry) continue;
             // the iteration's draws: a hit's (vertex, slots 0 and 1) or a new
             // sample's camera draws (vertex 0: theta and r of the defocus disk
             // at slots 2 and 3, else the pixel offsets at slots 0 and 1)
+            RT_ISA_MARK("draws");
             if (cam) rng.sample = (sie & 0xFFFFu) * F.S + s_j;
             Draws Dr;
             rng.pair(cam ? 0u : vertex, (cam && F.defocus) ? 1u : 0u, Dr.xi0, Dr.xi1);
@@ -2540,11 +2703,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             RT_DIAG_ONLY(const unsigned long long t_d = __builtin_amdgcn_s_memtime(); dg.cyc_refill += t_d - t_b1;
                          dg.cyc_draws += t_d - t_q;)
             if (!cam) {
+                RT_ISA_MARK("shade");
                 // ---- one ray_color level (camera.rs:275-325) at depth max_depth - vertex + 1
                 rng.begin(vertex);
                 rng.slot = 2;  // slots 0 and 1 are Dr
                 bool panic = false;
-                bool end_path = shade<TIER>(S, ray, beta, L, rng, true, T.hit, panic, Dr);
+                bool end_path;
+                if constexpr (TIER == TIER_BASIC && RT_SHADE_MERGED && !WIDE)  // (the wide variant spills 76 B/lane with it)
+                    end_path = shade_hit_basic(S, ray, beta, T.hit, panic, Dr);
+                else
+                    end_path = shade<TIER>(S, ray, beta, L, rng, true, T.hit, panic, Dr);
                 if (panic) {
                     ++n_panics;
                     end_path = true;
@@ -2559,6 +2727,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
                 }
                 RT_DIAG_ONLY(dg.cyc_shade += __builtin_amdgcn_s_memtime() - t_d;)
             } else {
+                RT_ISA_MARK("camera");
                 camera_ray(Dr);
                 RT_DIAG_ONLY(dg.cyc_refill += __builtin_amdgcn_s_memtime() - t_d;)
             }

@@ -235,6 +235,12 @@ struct SceneView {
     uint32_t world_root;
     uint32_t lights_root;  // REF_NONE = lights: None
     int32_t background_tex;  // -1 = black
+    // background_tex's kind when it is a sky gradient (BG_SKY), with its two
+    // colours copied here: the miss reads them with the launch parameters
+    // (scalar loads) instead of two dependent vector loads of the texture
+    // table in every wave iteration with a miss
+    int32_t bg_kind;
+    double bg_c0[3], bg_c1[3];  // BG_SKY: DTexture::color, color2
     uint32_t stack_need;     // max traversal stack entries (host-computed)
     uint32_t features;       // F_* of everything reachable from world/lights
     uint32_t n_nodes4;       // entries of nodes4
@@ -244,6 +250,8 @@ struct SceneView {
     // (make check, -DRT_CHECK) verifies every decoded ref against it
     uint32_t n_ref[16];
 };
+
+enum : int32_t { BG_NONE = 0, BG_SKY = 1, BG_OTHER = 2 };
 
 // Scene features; the launcher picks the smallest kernel tier covering them.
 enum : uint32_t {

@@ -403,6 +403,15 @@ static int32_t build_flat(rt_scene* s, int32_t world, int32_t lights, int32_t bg
     v.world_root = hw.world_root;
     v.lights_root = hw.lights_root;
     v.background_tex = bg;
+    v.bg_kind = rtk::BG_NONE;
+    std::memset(v.bg_c0, 0, sizeof v.bg_c0);
+    std::memset(v.bg_c1, 0, sizeof v.bg_c1);
+    if (bg >= 0 && (size_t)bg < hw.textures.size()) {
+        const rtk::DTexture& t = hw.textures[bg];
+        v.bg_kind = t.type == rtk::T_SKY ? rtk::BG_SKY : rtk::BG_OTHER;
+        if (v.bg_kind == rtk::BG_SKY)
+            for (int k = 0; k < 3; ++k) v.bg_c0[k] = t.color[k], v.bg_c1[k] = t.color2[k];
+    }
     v.stack_need = hw.stack_need;
     v.features = hw.features;
     v.n_nodes4 = (uint32_t)hw.nodes4.size();
