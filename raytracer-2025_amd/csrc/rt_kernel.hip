@@ -74,10 +74,13 @@ struct Diag {
     // basic tier: wave iterations with no lane able to walk a node (pure
     // sphere rounds), and the lanes with a queued sphere in them
     unsigned long long pure_rounds = 0, pure_lanes = 0, pure_max_pn = 0;
+    // ... per shading class (the 11 above): rounds in which it is present,
+    // and its lanes
+    unsigned long long cls_rounds[11] = {}, cls_lanes[11] = {};
 #endif
 };
 #ifdef RT_DIAG
-constexpr int RT_DIAG_N = 39;
+constexpr int RT_DIAG_N = 61;
 __device__ unsigned long long g_diag[RT_DIAG_N];
 #define RT_DIAG_ONLY(x) x
 #else
@@ -2945,8 +2948,16 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             }
             const unsigned long long act = __ballot(true);
             uint32_t kinds = 0;
-            for (uint32_t c = 0; c <= 10u; ++c) kinds += __ballot(cls == c) != 0ull ? 1u : 0u;
-            if (__lane_id() == (uint32_t)(__ffsll((long long)act) - 1)) {
+            const bool first = __lane_id() == (uint32_t)(__ffsll((long long)act) - 1);
+            for (uint32_t c = 0; c <= 10u; ++c) {
+                const unsigned long long bc = __ballot(cls == c);
+                kinds += bc != 0ull ? 1u : 0u;
+                if (first && bc) {
+                    ++dg.cls_rounds[c];
+                    dg.cls_lanes[c] += (unsigned long long)__popcll(bc);
+                }
+            }
+            if (first) {
                 ++dg.sh_rounds;
                 dg.sh_lanes += (unsigned long long)__popcll(act);
                 dg.sh_classes += kinds;
@@ -3037,6 +3048,10 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     atomicAdd(&g_diag[36], dg.pure_rounds);
     atomicAdd(&g_diag[37], dg.pure_lanes);
     atomicAdd(&g_diag[38], dg.pure_max_pn);
+    for (int k = 0; k < 11; ++k) {
+        atomicAdd(&g_diag[39 + k], dg.cls_rounds[k]);
+        atomicAdd(&g_diag[50 + k], dg.cls_lanes[k]);
+    }
 #endif
 #ifdef RT_WAVE_TRACE
     hist.flush();

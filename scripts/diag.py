@@ -37,7 +37,7 @@ elif wl == "c5":
 else:
     world, lights, cam = scenes.random_spheres(scene, 1920, spp)
 cam.render(world, lights, seed=1, want_srgb=False)  # warm-up + flatten
-buf = (ctypes.c_ulonglong * 39)()
+buf = (ctypes.c_ulonglong * 61)()
 lib.rt_diag_counters(buf, 1)
 _, _, st = cam.render(world, lights, seed=1, want_srgb=False)
 lib.rt_diag_counters(buf, 0)
@@ -90,6 +90,13 @@ out = {
     "pure_sphere_round_share": c[36] / c[3] if c[3] else None,
     "pure_round_lanes": c[37] / c[36] if c[36] else None,
     "pure_round_max_queued": c[38] / c[36] if c[36] else None,
-    "raw": c[:39],
+    # ... per class: the share of shading rounds it is present in, and its
+    # lanes per round when present
+    "shade_class_presence": {name: {"rounds_share": (c[39 + k] / c[33]) if c[33] else None,
+                                    "lanes_when_present": (c[50 + k] / c[39 + k]) if c[39 + k] else None}
+                             for k, name in enumerate(("miss", "lambertian_solid", "lambertian_checker",
+                                                       "lambertian_image", "lambertian_noise", "lambertian_sky",
+                                                       "metal", "dielectric", "diffuse_light", "isotropic", "other"))},
+    "raw": c[:61],
 }
 print(json.dumps(out, indent=1))
