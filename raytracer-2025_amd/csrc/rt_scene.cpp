@@ -1668,7 +1668,10 @@ uint32_t bvh4_convert(HostWorld& hw, uint32_t max_need, bool filter_spheres, siz
     const uint32_t sn = 1 + need(root);
     if (sn > max_need) return sn;
     if (out.size() > max_nodes) return UINT32_MAX;
-    if (!filter_spheres) {
+    // (RT_BVH4_TOP_BFS=0: the build's depth-first order throughout -- an A/B
+    // knob of the layout, read from the environment like rt_render.cpp's)
+    const char* bfs_env = std::getenv("RT_BVH4_TOP_BFS");
+    if (!filter_spheres && !(bfs_env && bfs_env[0] == '0')) {
         // the mesh / full tiers: the first BVH4_TOP nodes breadth-first from the
         // world's root BVH (levels 0-4 of a full 4-wide tree) take indices
         // 0 .. BVH4_TOP - 1, the rest keep the build's depth-first order after
