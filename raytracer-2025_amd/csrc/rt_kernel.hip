@@ -1892,6 +1892,41 @@ __device__ D3 emitted_tree(const SceneView& S, int mid, double u, double v, D3 p
 // ------------------------------------------------------------------ one ray_color level
 // camera.rs:275-325 at path vertex `vertex`; updates (ray, beta, L).  Returns
 // true when the path ends here (miss, no scatter, panic).
+// Deferred shading classes (full BVH tier, A/B lever): a lane whose hit is
+// a plain Lambertian with a texture kind in RT_SHADE_DEFER_TEX_MASK (a bit per
+// T_*) skips a shading round while fewer than RT_SHADE_DEFER_K such lanes are
+// ready, other lanes still walk, and the wave has deferred fewer than
+// RT_SHADE_DEFER_WAIT rounds in a row.  It keeps its hit, its RNG state and its
+// path and is shaded in a later round, with the same doubles (nothing it
+// computes depends on when).  0: off -- measured on C5 (64 spp, 4 reps, the
+// tier's product flags, RMSE 0): +0.5 % to +1.6 % kernel time, the noise
+// class's share of rounds 38 % -> 22 % but VALU exec density unchanged
+// (0.3383) and walk lane efficiency 0.628 -> 0.611
+// (profiles/r06/ab_shade_defer_t2flags_c5_64spp.json, density_c5_t2*.json).
+#ifndef RT_SHADE_DEFER
+#define RT_SHADE_DEFER 0
+#endif
+#ifndef RT_SHADE_DEFER_TEX_MASK
+#define RT_SHADE_DEFER_TEX_MASK (1u << T_NOISE)
+#endif
+#ifndef RT_SHADE_DEFER_K
+#define RT_SHADE_DEFER_K 12
+#endif
+#ifndef RT_SHADE_DEFER_WAIT
+#define RT_SHADE_DEFER_WAIT 3
+#endif
+// RT_SHADE_DEFER: the hit's material is a plain (non-emissive) Lambertian whose
+// texture kind is in RT_SHADE_DEFER_TEX_MASK
+__device__ __forceinline__ bool shade_deferrable(const SceneView& S, uint32_t ref) {
+    const uint32_t k = ref_kind(ref), i = ref_index(ref);
+    const int32_t m = k == K_SPHERE ? S.sphere_mat[i] : k == K_MSPHERE ? S.msph_mat[i]
+                    : (k == K_QUAD || k == K_TRI) ? S.planar_mat[i] : -1;
+    if (m < 0) return false;
+    const DMaterial& M = S.materials[m];
+    if (M.type != M_LAMBERTIAN || (M.flags & (MF_SOLID | MF_EMISSIVE))) return false;
+    return ((RT_SHADE_DEFER_TEX_MASK >> S.textures[M.tex].type) & 1u) != 0u;
+}
+
 template <int TIER>
 __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3& L, Rng& rng, bool hit_any,
                                       const HitInfo& h, bool& panic, const Draws& Dr = Draws{}) {
@@ -2461,6 +2496,11 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
     Diag dg;
     Trav<TIER> T;
     bool walking = false;
+    // RT_SHADE_DEFER (full BVH tier): this lane's finished walk waits for a later
+    // shading round; the wave's count of rounds deferred in a row
+    constexpr bool DEFER = RT_SHADE_DEFER && TIER == TIER_FULL;
+    bool deferred = false;
+    uint32_t defer_rounds = 0;
 #ifdef RT_WAVE_TRACE
     const uint32_t trace_lane = blockIdx.x * BLK + threadIdx.x;
     const unsigned long long trace_t0 = __builtin_amdgcn_s_memrealtime();
@@ -2854,7 +2894,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
 #ifdef RT_WAVE_TRACE
         hist.add(__ballot(!walking));
 #endif
-        if (!walking) {
+        if (!walking && !(DEFER && deferred)) {
             rng.begin(vertex);
             ++n_rays;
             trace_begin<TIER>(S, ray, T);
@@ -2918,10 +2958,23 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
         RT_DIAG_ONLY(const unsigned long long t_b1 = __builtin_amdgcn_s_memtime(); dg.cyc_trace += t_b1 - t_b0;)
         if constexpr (BATCH < 64 && tier_full(TIER)) {
             RT_DIAG_ONLY(const unsigned long long t_mb = __builtin_amdgcn_s_memtime();)
-            if (!walking) media_phase<TIER>(S, ray, T, stk, rng, med);
+            if (!walking && !(DEFER && deferred)) media_phase<TIER>(S, ray, T, stk, rng, med);
             RT_DIAG_ONLY(dg.cyc_media += __builtin_amdgcn_s_memtime() - t_mb;)
         }
-        if (BATCH < 64 && walking) {
+        if constexpr (DEFER) {
+            // wave-uniform: defer this round's candidates while few are ready,
+            // other lanes still walk, and the wave has not waited too long
+            const bool others = __ballot(walking) != 0ull;
+            const unsigned long long cm = __ballot(!walking && T.found && shade_deferrable(S, T.hit.ref));
+            if (cm != 0ull && others && __popcll(cm) < RT_SHADE_DEFER_K && defer_rounds < RT_SHADE_DEFER_WAIT) {
+                ++defer_rounds;
+                if ((cm >> __lane_id()) & 1ull) deferred = true;
+            } else {
+                defer_rounds = 0;
+                deferred = false;
+            }
+        }
+        if (BATCH < 64 && (walking || (DEFER && deferred))) {
             if constexpr (PARK) trace_park(T, pk);
             continue;
         }

@@ -8,6 +8,7 @@
 #   ab          interleaved A/B (scripts/ab.py AB_SPP AB_REPS AB_VARIANTS) on each of AB_WORKLOADS
 #   diag        diagnostic builds, one per "workload:lib:spp" in DIAG_RUNS (scripts/diag.py)
 #   ffp         whole-frame parity (scripts/full_frame_parity.py) for each of FFP (C5 at FFP_C5_SPP)
+#   density     VALU exec density (one --pmc pass) of each A/B variant in DENS_VARIANTS on DENS_WORKLOADS
 #   tail        1/8-shard rehearsal (scripts/tail_ab.py) for each of TAIL_WORKLOADS
 # Output under gpurun_out/$OUT.  Every GPU step has its own time limit; a
 # fault / abort / kill / timeout status (124, 134, 137, 139) or any failure
@@ -51,6 +52,15 @@ for step in ${STEPS:-tests}; do
         timeout -k 10 ${FFP_TIMEOUT:-600} python3 -u scripts/full_frame_parity.py $w $spp > $O/ffp_$w.jsonl 2> $O/ffp_$w.err
         rc=$?; [ $rc -eq 0 ] || { tail -5 $O/ffp_$w.err; stop "ffp $w" $rc; }
         tail -1 $O/ffp_$w.jsonl
+      done ;;
+    density)
+      # VALU exec density of A/B variants: one --pmc pass per (workload, variant)
+      for w in ${DENS_WORKLOADS:-c5}; do
+        for v in ${DENS_VARIANTS:-base}; do
+          RT_MI355X_LIB=raytracer-2025_amd/librt_ab_$v.so timeout -k 10 300 timeout -s KILL 290 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d $O/dens_${w}_$v -o run -- python3 bench.py --workload $w --steps 1 --warmup 1 --spp ${DENS_SPP:-64} --no-cpu-baseline --no-host-rate > $O/dens_${w}_$v.log 2>&1
+          rc=$?; [ $rc -eq 0 ] || { tail -5 $O/dens_${w}_$v.log; stop "density $w $v" $rc; }
+          python3 scripts/exec_density.py $O/dens_${w}_$v/run_counter_collection.csv $w $v | tee $O/dens_${w}_$v.json
+        done
       done ;;
     tail)
       for w in ${TAIL_WORKLOADS:-c2}; do
