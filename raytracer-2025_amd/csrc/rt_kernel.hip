@@ -357,7 +357,7 @@ __device__ __forceinline__ bool sphere_t(D3 c, double radius, const Ray& r, doub
     const double cc = len2(oc) - radius * radius;
     const double disc = h * h - a * cc;
     if (disc < 0.0) return false;
-    const double sq = sqrt(disc);
+    const double sq = k_sqrt(disc);
     double root = (h - sq) / a;
     if (!(root >= tmin && root <= tmax)) {
         root = (h + sq) / a;
@@ -383,7 +383,7 @@ __device__ __forceinline__ bool sphere_t_inv(D3 c, double radius, const Ray& r, 
     const double cc = len2(oc) - radius * radius;
     const double disc = h * h - a * cc;
     if (disc < 0.0) return false;
-    const double sq = sqrt(disc);
+    const double sq = k_sqrt(disc);
     double root = div_a(h - sq, a, inva);
     if (!(root >= tmin && root <= tmax)) {
         root = div_a(h + sq, a, inva);
@@ -822,7 +822,7 @@ __device__ __forceinline__ bool boundary_onepass(const SceneView& S, const DMedi
         const double cc = len2(oc) - s4.w * s4.w;
         const double disc = h * h - a * cc;
         if (disc < 0.0) return false;
-        const double sq = sqrt(disc);
+        const double sq = k_sqrt(disc);
         const double rn = div_a(h - sq, a, inva), rf = div_a(h + sq, a, inva);
         auto pick = [&](double lo, double& t) {
             if (rn >= lo && rn <= PINF) t = rn;
@@ -1676,7 +1676,7 @@ __device__ double light_pdf_one(const SceneView& S, uint32_t ref, D3 o, D3 d) {
         const double4 s = S.spheres[idx];
         if (!sphere_t(d3(s.x, s.y, s.z), s.w, r, len2(d), 1e-8, __builtin_huge_val(), t)) return 0.0;
         const double dist_squared = len2(d3(s.x, s.y, s.z) - o);
-        const double ctm = sqrt(1.0 - s.w * s.w / dist_squared);
+        const double ctm = k_sqrt(1.0 - s.w * s.w / dist_squared);
         if (isnan(ctm)) return 1.0 / (4.0 * PI);
         return 1.0 / (2.0 * PI * (1.0 - ctm));
     }
@@ -1719,10 +1719,10 @@ __device__ __forceinline__ D3 light_random_one(const SceneView& S, uint32_t ref,
     bool ok1, ok2;
     const D3 nd = unit(direction, ok1);
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
-    const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
+    const double y = 1.0 + r2 * (k_sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
     double sphi, cphi;
     k_sincos_2pi(r1, &sphi, &cphi);  // phi = 2.0 * PI * r1
-    const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
+    const double x = cphi * k_sqrt(1.0 - y * y), z = sphi * k_sqrt(1.0 - y * y);
     const D3 wv = onb_world(nd, d3(x, y, z), ok2);
     bool ok3;
     const D3 res = unit(wv, ok3);
@@ -1759,7 +1759,7 @@ __device__ double light_pdf_leaf(const SceneView& S, uint32_t ref, D3 o, D3 d) {
     double t;
     if (!sphere_t(d3(s.x, s.y, s.z), s.w, r, len2(d), 1e-8, __builtin_huge_val(), t)) return 0.0;
     const double dist_squared = len2(d3(s.x, s.y, s.z) - o);
-    const double ctm = sqrt(1.0 - s.w * s.w / dist_squared);
+    const double ctm = k_sqrt(1.0 - s.w * s.w / dist_squared);
     if (isnan(ctm)) return 1.0 / (4.0 * PI);
     return 1.0 / (2.0 * PI * (1.0 - ctm));
 }
@@ -1816,10 +1816,10 @@ __device__ D3 light_random_tree(const SceneView& S, uint32_t ref, D3 o, Rng& rng
         bool ok1, ok2, ok3;
         const D3 nd = unit(direction, ok1);
         const double r1 = rng.next(ovf), r2 = rng.next(ovf);
-        const double y = 1.0 + r2 * (sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
+        const double y = 1.0 + r2 * (k_sqrt(1.0 - s.w * s.w / distance_squared) - 1.0);
         double sphi, cphi;
         k_sincos_2pi(r1, &sphi, &cphi);  // phi = 2.0 * PI * r1
-        const double x = cphi * sqrt(1.0 - y * y), z = sphi * sqrt(1.0 - y * y);
+        const double x = cphi * k_sqrt(1.0 - y * y), z = sphi * k_sqrt(1.0 - y * y);
         const D3 res = unit(onb_world(nd, d3(x, y, z), ok2), ok3);
         ok = ok1 && ok2 && ok3;
         return res;
@@ -1840,7 +1840,7 @@ __device__ __forceinline__ D3 random_unit_vector(Rng& rng, uint32_t& ovf) {
     const double r1 = rng.next(ovf), r2 = rng.next(ovf);
     double sn, cs;
     k_sincos_2pi(r1, &sn, &cs);
-    const double s = sqrt(r2 * (1.0 - r2));
+    const double s = k_sqrt(r2 * (1.0 - r2));
     return d3(cs * 2.0 * s, sn * 2.0 * s, 1.0 - 2.0 * r2);
 }
 
@@ -2048,7 +2048,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             if constexpr (!HOIST) {
                 ruv = random_unit_vector(rng, ovf);
             } else {
-                const double s = sqrt(xi1 * (1.0 - xi1));
+                const double s = k_sqrt(xi1 * (1.0 - xi1));
                 ruv = d3(cs0 * 2.0 * s, sn0 * 2.0 * s, 1.0 - 2.0 * xi1);
             }
             beta = beta * d3(M.albedo[0], M.albedo[1], M.albedo[2]);
@@ -2061,7 +2061,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
             const D3 ud = unit(ray.d, ok);
             if (!ok) panic = true;
             const double cos_theta = fmin(dot(-ud, n), 1.0);
-            const double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+            const double sin_theta = k_sqrt(1.0 - cos_theta * cos_theta);
             bool do_reflect = ri * sin_theta > 1.0;
             if (!do_reflect) {  // Schlick (material.rs:110-114); the draw only when refraction is possible
                 const double r0 = (1.0 - ri) / (1.0 + ri);
@@ -2075,7 +2075,7 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                 dir = reflect(ud, n);
             } else {  // vec3.rs:345-354
                 const D3 perp = ri * (ud + cos_theta * n);
-                const double pl = sqrt(1.0 - len2(perp));
+                const double pl = k_sqrt(1.0 - len2(perp));
                 if (isnan(pl)) panic = true;
                 dir = perp + (-pl * n);
             }
@@ -2112,8 +2112,8 @@ __device__ __forceinline__ bool shade(const SceneView& S, Ray& ray, D3& beta, D3
                     r2 = rng.next(ovf);
                     k_sincos_2pi(r1, &sn, &cs);
                 }
-                const double sr2 = sqrt(r2);
-                dir = onb_world(n, d3(sn * sr2, sqrt(1.0 - r2), cs * sr2), ok);
+                const double sr2 = k_sqrt(r2);
+                dir = onb_world(n, d3(sn * sr2, k_sqrt(1.0 - r2), cs * sr2), ok);
             } else {
                 dir = random_unit_vector(rng, ovf);
             }
@@ -2213,9 +2213,9 @@ __device__ __forceinline__ bool shade_hit_basic(const SceneView& S, Ray& ray, D3
         cosd = fmin(dot(-uA, n), 1.0);
         xB1 = 1.0 - cosd * cosd;
     }
-    const double sB1 = sqrt(xB1);
+    const double sB1 = k_sqrt(xB1);
     double sB2 = 0.0;
-    if (cls == LAMB) sB2 = sqrt(1.0 - xi1);
+    if (cls == LAMB) sB2 = k_sqrt(1.0 - xi1);
     // ---- C
     D3 vC = ray.d;
     if (cls == LAMB) {  // onb_world: v.x u + v.y n + v.z w (onb.rs:34-38)
@@ -2270,7 +2270,7 @@ __device__ __forceinline__ bool shade_hit_basic(const SceneView& S, Ray& ray, D3
         dir = reflect(uA, n);
     } else {  // vec3.rs:345-354
         const D3 perp = ri * (uA + cosd * n);
-        const double pl = sqrt(1.0 - len2(perp));
+        const double pl = k_sqrt(1.0 - len2(perp));
         if (isnan(pl)) panic = true;
         dir = perp + (-pl * n);
     }
@@ -2627,7 +2627,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
 #ifndef RT_MEASURE_NOCAMPAIR
                 rng.pair(0u, 0u, xi0, xi1);
 #endif
-                const double rr = sqrt(Dr.xi1);
+                const double rr = k_sqrt(Dr.xi1);
                 origin = (F.center + ((rr * Dr.cs) * F.disk_u)) + ((rr * Dr.sn) * F.disk_v);
             }
             const double ox = (((double)s_i + xi0) * F.recip_sqrt_spp) - 0.5;
@@ -2869,7 +2869,7 @@ __global__ void __launch_bounds__(TIER == TIER_BASIC ? RT_BLOCK_BASIC : RT_BLOCK
             D3 origin = F.center;
             if (F.defocus) {
                 const double xt = rng.next(ovf);  // theta = 0.0 + (2.0 * PI - 0.0) * xt = 2.0 * PI * xt (vec3.rs:63-69)
-                const double rr = sqrt(rng.next(ovf));
+                const double rr = k_sqrt(rng.next(ovf));
                 double sn, cs;
                 k_sincos_2pi(xt, &sn, &cs);
                 origin = (F.center + ((rr * cs) * F.disk_u)) + ((rr * sn) * F.disk_v);
@@ -3359,7 +3359,7 @@ __global__ void __launch_bounds__(256) rt_math_kernel(int fn, int impl, const do
             case 6: r = rtcr::atan2(x, y); break;
             case 8: rtcr::sincos_2pi(x, &s, &c), r = s; break;
             case 9: rtcr::sincos_2pi(x, &s, &c), r = c; break;
-            default: r = sqrt(x); break;
+            default: r = k_sqrt(x); break;  // the path's square root (RT_FAST_SQRT)
         }
     } else {
         switch (fn) {

@@ -29,8 +29,36 @@ __device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y
 __device__ __forceinline__ D3 cross(D3 a, D3 b) {
     return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// f64 square root, the same double as sqrt(x) (IEEE, correctly rounded).
+// LLVM lowers sqrt to v_rsq_f64 and two Newton-Raphson corrections on x scaled
+// by 2^256 when x < 2^-767, and then selects x itself for +-0 and +inf.  For x in
+// [2^-767, inf) the scale is 2^0 and the select keeps the Newton result, so that
+// sequence without them is the same instructions on the same values.
+// RT_FAST_SQRT takes it when every active lane's x is in that range (a
+// wave-uniform branch), else sqrt(x) for the wave: C2 -1.1 % kernel time, C4
+// -0.15 %, C5 +-0 (A/B, RMSE 0: profiles/r06/ab_fast_sqrt_c*.json; bit-equal to
+// IEEE sqrt on every binade and on mixed waves, tests/test_sqrt_gpu.py).
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1
+#endif
+__device__ __forceinline__ double k_sqrt(double x) {
+#if RT_FAST_SQRT
+    if (__builtin_expect(__ballot(!(x >= 0x1p-767 && x < __builtin_huge_val())) == 0ull, 1)) {
+        const double y = __builtin_amdgcn_rsq(x);
+        double g = x * y, h = y * 0.5;
+        const double r = __builtin_fma(-h, g, 0.5);
+        g = __builtin_fma(g, r, g);
+        h = __builtin_fma(h, r, h);
+        double d = __builtin_fma(-g, g, x);
+        g = __builtin_fma(d, h, g);
+        d = __builtin_fma(-g, g, x);
+        return __builtin_fma(d, h, g);
+    }
+#endif
+    return sqrt(x);
+}
 __device__ __forceinline__ double len2(D3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-__device__ __forceinline__ double len(D3 a) { return sqrt(len2(a)); }
+__device__ __forceinline__ double len(D3 a) { return k_sqrt(len2(a)); }
 __device__ __forceinline__ bool finite3(D3 v) { return isfinite(v.x) && isfinite(v.y) && isfinite(v.z); }
 // UnitVec3::from_vec3 (vec3.rs:299-306): v / |v|, ok = all finite
 __device__ __forceinline__ D3 unit(D3 v, bool& ok) {
